@@ -1,0 +1,125 @@
+/*
+ * nf4_dequant.h -- C ABI of the MI355X (gfx950) NF4 double-dequantization path.
+ *
+ * Library: nf4_triton_dequantization_amd/_lib/libnf4dq.so (hipcc, gfx950).
+ * Every entry point is asynchronous on the given HIP stream, allocates nothing,
+ * keeps no global mutable state, and returns 0 or an NF4DQ_* error code.
+ * Pointers are device pointers unless stated otherwise; `hip_stream` is a
+ * hipStream_t (NULL = the null stream).
+ *
+ * Reference interfaces replaced (felipemcoelho/nf4-triton-dequantization,
+ * file nf4_triton_dequantization/kernel_optimized.py):
+ *   nf4_dequant_ref    <- _triton_dequantize_main :142-205 launching
+ *                         _nf4_dequantize_kernel_final :11-110 (uint8 absmax,
+ *                         double dequant; wrap/truncate rules :173-186)
+ *   nf4_dequant_single <- the non-uint8 absmax branch :166-167 -> :273-274
+ *   nf4_dequant_ref_batched <- benchmark.py:68-84 (several Linear4bit weights
+ *                         per step) folded into one launch
+ *   nf4_dequant_bnb / nf4_dequant_bnb_single <- bitsandbytes dequantize_4bit
+ *                         semantics; the reference
+ *                         never implements these, they are parity-unpinned.
+ */
+#ifndef NF4_DEQUANT_H_
+#define NF4_DEQUANT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Output dtypes (quant_state.dtype, kernel_optimized.py:123, :189). */
+#define NF4DQ_F16 0
+#define NF4DQ_BF16 1
+#define NF4DQ_F32 2
+
+/* Return codes. HIP launch failures are NF4DQ_ERR_HIP_BASE + hipError_t. */
+#define NF4DQ_OK 0
+#define NF4DQ_ERR_ARG 1        /* null pointer, bad dtype, negative size      */
+#define NF4DQ_ERR_SHAPE 2      /* sizes the reference would reject (view fails) */
+#define NF4DQ_ERR_TOO_LARGE 3  /* a single matrix beyond 2^31 packed bytes    */
+#define NF4DQ_ERR_HIP_BASE 1000
+
+/* Reference double dequant of one Linear4bit weight into row-major out[m][n].
+ *   packed   uint8[packed_len]  two NF4 codes per byte, high nibble first;
+ *                               row r starts at r*(packed_len/m)
+ *   absmax_q uint8[nb]          per (row, 64-column block); index wraps mod nb
+ *   absmax2  fp32[n2]           index r*ceil(bpr/4) + block/4, wraps mod n2
+ * out[r][c] = RNE(NF4[nib] * ((float)absmax_q[.] / 127.0f * absmax2[.])).
+ * Errors: packed_len % m != 0 or packed_len/m < ceil(n/2) -> NF4DQ_ERR_SHAPE. */
+int nf4_dequant_ref(const uint8_t* packed, int64_t packed_len,
+                    const uint8_t* absmax_q, int64_t nb,
+                    const float* absmax2, int64_t n2,
+                    void* out, int32_t out_dtype, int64_t m, int64_t n,
+                    void* hip_stream);
+
+/* Single-quant branch: absmax fp32[absmax_len] viewed as [m, absmax_len/m],
+ * scale of (r, b) = absmax[r*(absmax_len/m) + b]. */
+int nf4_dequant_single(const uint8_t* packed, int64_t packed_len,
+                       const float* absmax, int64_t absmax_len,
+                       void* out, int32_t out_dtype, int64_t m, int64_t n,
+                       void* hip_stream);
+
+/* One matrix of a batched call (host memory; copied into kernel arguments). */
+typedef struct nf4_matrix_desc {
+    const uint8_t* packed;
+    int64_t packed_len;
+    const uint8_t* absmax_q;
+    int64_t nb;
+    const float* absmax2;
+    int64_t n2;
+    void* out;
+    int64_t m;
+    int64_t n;
+} nf4_matrix_desc;
+
+/* Dequantize `count` matrices (same out_dtype) with as few launches as the
+ * kernel-argument budget allows (NF4DQ_BATCH_MAX matrices per launch). */
+#define NF4DQ_BATCH_MAX 24
+int nf4_dequant_ref_batched(const nf4_matrix_desc* descs, int32_t count,
+                            int32_t out_dtype, void* hip_stream);
+
+/* bitsandbytes nested semantics over the flat element stream:
+ *   absmax_f32[i] = code2[absmax_q[i]] * absmax2[i / blocksize2] + offset
+ *   out[k]        = RNE(NF4[nib(k)] * absmax_f32[k / blocksize])
+ * blocksize and blocksize2 must be powers of two, blocksize >= 64. */
+int nf4_dequant_bnb(const uint8_t* packed, const uint8_t* absmax_q, int64_t nb,
+                    const float* code2, const float* absmax2, int64_t n2,
+                    float offset, void* out, int32_t out_dtype, int64_t numel,
+                    int32_t blocksize, int32_t blocksize2, void* hip_stream);
+
+/* bitsandbytes single-level (compress_statistics=False): fp32 absmax per block. */
+int nf4_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t nabs,
+                           void* out, int32_t out_dtype, int64_t numel,
+                           int32_t blocksize, void* hip_stream);
+
+/* Launch tuning (bench/tuning only; the entry points above use defaults).
+ * tile_dwords: 4 or 8 packed dwords per lane per tile; blocks_per_cu: grid cap
+ * per CU (0 = one workgroup per 4 tiles, no cap); nontemporal: 0/1 streaming
+ * (nt) output stores; flags: NF4DQ_CFG_* bits. */
+#define NF4DQ_CFG_NT_LOADS 1   /* nt cache policy on the packed-weight loads */
+typedef struct nf4_launch_cfg {
+    int32_t tile_dwords;
+    int32_t blocks_per_cu;
+    int32_t nontemporal;
+    int32_t flags;
+} nf4_launch_cfg;
+
+int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len,
+                        const uint8_t* absmax_q, int64_t nb,
+                        const float* absmax2, int64_t n2,
+                        void* out, int32_t out_dtype, int64_t m, int64_t n,
+                        const nf4_launch_cfg* cfg, void* hip_stream);
+
+/* Human-readable text for a return code (static storage). */
+const char* nf4_strerror(int code);
+
+/* Library version string, e.g. "nf4dq 0.1.0 gfx950". */
+const char* nf4_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NF4_DEQUANT_H_ */

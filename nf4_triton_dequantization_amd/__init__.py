@@ -1,0 +1,23 @@
+"""MI355X-native NF4 double-dequantization (gfx950 HIP kernels behind a C ABI).
+
+Public API mirrors the reference package ``nf4_triton_dequantization``
+(/root/reference/nf4_triton_dequantization/__init__.py:7-12):
+
+    from nf4_triton_dequantization_amd import triton_dequantize_nf4, reset_triton_dequantize_state
+
+The alias package ``nf4_triton_dequantization`` (repo root) re-exports the same
+names so existing callers (benchmark.py:11) import it unchanged.
+"""
+from .kernel import (  # noqa: F401
+    dequantize_nf4_bnb,
+    dequantize_nf4_into,
+    dequantize_nf4_many,
+    reset_triton_dequantize_state,
+    triton_dequantize_nf4,
+)
+from .bnb_layout import Linear4bit, Params4bit, QuantState, quantize_nf4  # noqa: F401
+
+__all__ = ["triton_dequantize_nf4", "reset_triton_dequantize_state", "dequantize_nf4_many",
+           "dequantize_nf4_bnb", "dequantize_nf4_into", "Linear4bit", "Params4bit", "QuantState",
+           "quantize_nf4"]
+__version__ = "0.1.0"

@@ -1,0 +1,107 @@
+"""ctypes binding of the C ABI in include/nf4_dequant.h (libnf4dq.so, gfx950).
+
+The library is loaded after ``import torch`` so that it binds to the HIP runtime
+torch already mapped (same SONAME ``libamdhip64.so.7``): one HIP runtime per
+process.  There is no fallback: if the library is missing or fails to load,
+``lib()`` raises, and so does every product entry point that needs it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libnf4dq.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nf4_dequant.h")
+
+F16 = 0
+BF16 = 1
+F32 = 2
+
+OK = 0
+ERR_ARG = 1
+ERR_SHAPE = 2
+ERR_TOO_LARGE = 3
+ERR_HIP_BASE = 1000
+
+BATCH_MAX = 24
+
+
+class MatrixDesc(ctypes.Structure):
+    """nf4_matrix_desc (include/nf4_dequant.h)."""
+
+    _fields_ = [
+        ("packed", ctypes.c_void_p),
+        ("packed_len", ctypes.c_int64),
+        ("absmax_q", ctypes.c_void_p),
+        ("nb", ctypes.c_int64),
+        ("absmax2", ctypes.c_void_p),
+        ("n2", ctypes.c_int64),
+        ("out", ctypes.c_void_p),
+        ("m", ctypes.c_int64),
+        ("n", ctypes.c_int64),
+    ]
+
+
+class LaunchCfg(ctypes.Structure):
+    """nf4_launch_cfg (include/nf4_dequant.h)."""
+
+    _fields_ = [
+        ("tile_dwords", ctypes.c_int32),
+        ("blocks_per_cu", ctypes.c_int32),
+        ("nontemporal", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+    ]
+
+
+CFG_NT_LOADS = 1
+
+
+# name -> (restype, argtypes); every symbol include/nf4_dequant.h declares.
+_P, _I64, _I32, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_float
+SIGNATURES = {
+    "nf4_dequant_ref": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I32, _I64, _I64, _P]),
+    "nf4_dequant_single": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I32, _I64, _I64, _P]),
+    "nf4_dequant_ref_batched": (ctypes.c_int, [ctypes.POINTER(MatrixDesc), _I32, _I32, _P]),
+    "nf4_dequant_bnb": (ctypes.c_int, [_P, _P, _I64, _P, _P, _I64, _F, _P, _I32, _I64, _I32, _I32, _P]),
+    "nf4_dequant_bnb_single": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _I64, _I32, _P]),
+    "nf4_dequant_ref_cfg": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I32, _I64, _I64,
+                                           ctypes.POINTER(LaunchCfg), _P]),
+    "nf4_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "nf4_version": (ctypes.c_char_p, []),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"nf4 HIP library not built: {LIB_PATH} is missing "
+                    "(run `python __graft_entry__.py build` or `make -C nf4_triton_dequantization_amd`)")
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+    return _lib
+
+
+def strerror(code: int) -> str:
+    return lib().nf4_strerror(int(code)).decode()
+
+
+def check(code: int, what: str) -> None:
+    if code != OK:
+        raise RuntimeError(f"{what} failed: {strerror(code)} (code {code})")

@@ -1,0 +1,727 @@
+// nf4_dequant.hip -- MI355X (gfx950 / CDNA4) NF4 double-dequantization kernels
+// and the C ABI declared in include/nf4_dequant.h.
+//
+// What it replaces: the Triton kernel _nf4_dequantize_kernel_final
+// (reference nf4_triton_dequantization/kernel_optimized.py:11-110) and its
+// launcher _triton_dequantize_main (:142-205).  Semantics are the reference
+// fallback's (_aggressive_pytorch_t4, :208-314), bit for bit; see
+// oracle/nf4_oracle.c for the CPU restatement and DESIGN.md for the layout.
+//
+// Design (bandwidth-bound: 0.5 B in + 2 B out per element, no MFMA):
+//  * "flat" kernel: whenever no 64-column block straddles a row (n % 64 == 0 and
+//    the packed rows are dense) the packed weight is one byte stream.  A wave
+//    owns a tile of 256*U packed bytes; lane l loads dword j at
+//    tile + 256*j + 4*l, so each load instruction reads 256 contiguous bytes and
+//    each of the U 16-byte output stores writes 1 KiB contiguous per wave:
+//    every HBM line is written whole by one store instruction.  Loads and
+//    stores are buffer instructions (range-checked: partial tiles need no
+//    predicates), output stores are non-temporal (written once, streamed),
+//    and the persistent wave loop is software-pipelined: the next tile's loads
+//    are in flight while the current tile is decoded and stored.
+//  * one lane per 64-element block computes the block's scale (absmax byte,
+//    nested absmax, IEEE fp32 division by 127 -- never a reciprocal), and the
+//    eight lanes that own the block's dwords fetch it with ds_bpermute.
+//  * the 16-entry NF4 table sits in LDS: 16 consecutive fp32 = 16 distinct
+//    banks, repeated indices broadcast, so the lookups are conflict-free.
+//  * fp32 -> bf16/fp16 through v_cvt_pk_{bf16,f16}_f32 (round to nearest even),
+//    two outputs per instruction, high nibble -> even column (fp32 output, as
+//    quant_state.dtype = torch.float32 asks, is stored unrounded).
+//  * batched: up to NF4DQ_BATCH_MAX matrices per launch in the kernel
+//    arguments; a wave finds its matrix by scanning scalar tile offsets.
+//  * "rows" kernels: any other shape (partial blocks, padded rows, odd n) --
+//    one thread per packed byte, 64-bit indexing, same arithmetic.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nf4_dequant.h"
+
+namespace {
+
+// NF4 code points as the fp32 bit patterns of kernel_optimized.py:234-239.
+__constant__ uint32_t kNf4Bits[16] = {
+    0xbf800000u, 0xbf3239b1u, 0xbf066b30u, 0xbeca32a0u,
+    0xbe91a24du, 0xbe3d353fu, 0xbdba7871u, 0x00000000u,
+    0x3da2faffu, 0x3e24cae3u, 0x3e7c04ddu, 0x3ead033au,
+    0x3ee1a4b8u, 0x3f1007abu, 0x3f3913b3u, 0x3f800000u,
+};
+
+enum Mode : int { kRef = 0, kSingle = 1, kBnb = 2, kBnbSingle = 3 };
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Division by a run-time constant for n < 2^31: q = (umulhi(n, mul) + n) >> shift.
+struct FastDiv {
+    uint32_t d, mul, shift;
+};
+
+FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f{d, 0u, 0u};
+    uint32_t s = 0;
+    while (s < 32 && (uint64_t(1) << s) < d) ++s;
+    f.shift = s;
+    f.mul = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << s) - d)) / d + 1);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    return (__umulhi(n, f.mul) + n) >> f.shift;
+}
+__device__ __forceinline__ uint32_t fmodu(uint32_t n, const FastDiv& f) {
+    return n - fdiv(n, f) * f.d;
+}
+
+// Kernel-argument image of one matrix on the flat path.
+struct Desc {
+    const uint32_t* packed;  // dense packed stream (4-byte aligned)
+    const uint8_t* a1;       // uint8 absmax (ref, bnb)
+    const float* a2;         // nested absmax (ref, bnb) or fp32 absmax (single modes)
+    const float* code2;      // bnb nested code book (256 fp32)
+    u32x4* out;              // 16-byte aligned output
+    float offset;            // bnb offset
+    uint32_t nbytes;         // packed bytes (multiple of 4)
+    uint32_t tile_begin;     // first tile of this matrix within the launch
+    uint32_t groups;         // ceil(bpr/4) (ref)
+    FastDiv nb;              // ref: modulus of A1 index
+    FastDiv n2;              // ref: modulus of A2 index; single: .d = row stride
+    FastDiv bpr;             // blocks per row
+    uint32_t blk_shift;      // log2(bytes per scale block)
+    uint32_t blk2_shift;     // bnb: log2(blocksize2)
+};
+
+template <int MAXB>
+struct Batch {
+    Desc d[MAXB];
+    uint32_t count;
+    uint32_t total_tiles;
+};
+
+// Keep an fp32 product opaque to the backend: without this, hipcc folds
+// fptrunc(fmul) into v_fma_mix*_f16(a, b, +0), which rounds once instead of
+// twice (fp32 product, then fp16 -- the reference's order) and turns -0 into +0.
+__device__ __forceinline__ float opaque(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+template <int DT>
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+    if constexpr (DT == NF4DQ_F16) {
+        lo = opaque(lo);
+        hi = opaque(hi);
+    }
+    f32x2 v = {lo, hi};
+    if constexpr (DT == NF4DQ_BF16) {
+        return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+    } else {
+        return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
+    }
+}
+
+// Scalar store of one output element (rows kernels).
+template <int DT>
+__device__ __forceinline__ void store1(void* out, int64_t i, float x) {
+    if constexpr (DT == NF4DQ_BF16) {
+        reinterpret_cast<__bf16*>(out)[i] = (__bf16)x;
+    } else if constexpr (DT == NF4DQ_F16) {
+        reinterpret_cast<_Float16*>(out)[i] = (_Float16)opaque(x);
+    } else {
+        reinterpret_cast<float*>(out)[i] = x;
+    }
+}
+
+// Scale of flat block g (reference rules in the header of oracle/nf4_oracle.c).
+template <int MODE>
+__device__ __forceinline__ float block_scale(const Desc& D, uint32_t g) {
+    if constexpr (MODE == kRef) {
+        const float q = (float)D.a1[fmodu(g, D.nb)];
+        const uint32_t r = fdiv(g, D.bpr);
+        const uint32_t b = g - r * D.bpr.d;
+        const float s2 = D.a2[fmodu(r * D.groups + (b >> 2), D.n2)];
+        return (q / 127.0f) * s2;  // IEEE division (:45, :270), then fp32 multiply
+    } else if constexpr (MODE == kSingle) {
+        const uint32_t r = fdiv(g, D.bpr);
+        const uint32_t b = g - r * D.bpr.d;
+        return D.a2[r * D.n2.d + b];
+    } else if constexpr (MODE == kBnb) {
+        return D.code2[D.a1[g]] * D.a2[g >> D.blk2_shift] + D.offset;
+    } else {
+        return D.a2[g];
+    }
+}
+
+constexpr int kWg = 256;  // 4 waves
+constexpr int kWavesPerWg = kWg / 64;
+
+// Cache-policy bits of the buffer instructions (aux operand): 2 = nt (streaming).
+constexpr int kAuxNt = 2;
+constexpr int kRsrcFlags = 0x00020000;  // raw buffer, dword format (gfx950)
+
+template <int DT>
+constexpr uint32_t out_bytes_per_packed_byte() { return DT == NF4DQ_F32 ? 8u : 4u; }
+
+// Raw inputs of one wave-tile, loaded ahead of use (software pipeline stage 1).
+template <int U>
+struct TileIn {
+    uint32_t w[U];  // U packed dwords of this lane
+    uint32_t a1;    // raw absmax byte of this lane's scale block (ref / bnb)
+    float a2;       // nested absmax (ref / bnb) or fp32 absmax (single modes)
+    float c2;       // bnb: code2[a1] (loaded after a1)
+};
+
+// Issue the loads of tile `base` (packed bytes) of matrix D.  Buffer loads
+// outside the matrix return 0, so partial tiles need no predicates.
+template <int MODE, int U, int AUXL>
+__device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rsrc_t rp, uint32_t base,
+                                               uint32_t lane) {
+    TileIn<U> in;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        in.w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, base + 256u * j + 4u * lane, 0, AUXL);
+    }
+    constexpr uint32_t kTileBytes = 256u * U;
+    const uint32_t bsh = D.blk_shift;
+    const uint32_t bpt = kTileBytes >> bsh;  // 0 when one block spans the tile
+    uint32_t g = (base >> bsh) + (bpt ? (lane & (bpt - 1u)) : 0u);
+    const uint32_t nblk = (D.nbytes + (1u << bsh) - 1u) >> bsh;
+    g = g < nblk ? g : nblk - 1u;  // lanes past the end read a valid block; their stores drop
+    if constexpr (MODE == kRef) {
+        in.a1 = D.a1[fmodu(g, D.nb)];
+        const uint32_t r = fdiv(g, D.bpr);
+        const uint32_t b = g - r * D.bpr.d;
+        in.a2 = D.a2[fmodu(r * D.groups + (b >> 2), D.n2)];
+    } else if constexpr (MODE == kSingle) {
+        const uint32_t r = fdiv(g, D.bpr);
+        const uint32_t b = g - r * D.bpr.d;
+        in.a2 = D.a2[r * D.n2.d + b];
+    } else if constexpr (MODE == kBnb) {
+        in.a1 = D.a1[g];
+        in.a2 = D.a2[g >> D.blk2_shift];
+    } else {
+        in.a2 = D.a2[g];
+    }
+    return in;
+}
+
+// Stage 2: scale of this lane's block, ds_bpermute to the dword owners, decode,
+// round, and U 16-byte stores (fp32: 2U) -- each wave store instruction writes
+// 1 KiB contiguous; stores past the end of the matrix are dropped by the buffer
+// range check.
+template <int DT, int MODE, int U, int AUXS>
+__device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_t ro, const float* lut,
+                                            const TileIn<U>& in, uint32_t base, uint32_t lane) {
+    float s;
+    if constexpr (MODE == kRef) {
+        s = ((float)in.a1 / 127.0f) * in.a2;  // IEEE division (:45, :270), then fp32 multiply
+    } else if constexpr (MODE == kBnb) {
+        s = D.code2[in.a1] * in.a2 + D.offset;
+    } else {
+        s = in.a2;
+    }
+    const uint32_t bsh = D.blk_shift;
+    constexpr uint32_t kOB = out_bytes_per_packed_byte<DT>();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t rel = 256u * j + 4u * lane;
+        const float sj = __shfl(s, (int)(rel >> bsh), 64);
+        const uint32_t w = in.w[j];
+        const uint32_t hi4 = (w >> 2) & 0x3C3C3C3Cu;
+        const uint32_t lo4 = (w << 2) & 0x3C3C3C3Cu;
+        const char* t = reinterpret_cast<const char*>(lut);
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[2 * k] = *reinterpret_cast<const float*>(t + ((hi4 >> (8 * k)) & 0xFFu)) * sj;
+            v[2 * k + 1] = *reinterpret_cast<const float*>(t + ((lo4 >> (8 * k)) & 0xFFu)) * sj;
+        }
+        const uint32_t ob = (base + rel) * kOB;
+        if constexpr (DT == NF4DQ_F32) {
+            u32x4 o0 = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+            u32x4 o1 = {__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
+            __builtin_amdgcn_raw_buffer_store_b128(o0, ro, ob, 0, AUXS);
+            __builtin_amdgcn_raw_buffer_store_b128(o1, ro, ob + 16u, 0, AUXS);
+        } else {
+            u32x4 o = {pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7])};
+            __builtin_amdgcn_raw_buffer_store_b128(o, ro, ob, 0, AUXS);
+        }
+    }
+}
+
+template <int MAXB>
+__device__ __forceinline__ uint32_t find_matrix(const Batch<MAXB>& bt, uint32_t t, uint32_t k) {
+    if constexpr (MAXB > 1) {
+        while (k + 1 < bt.count && t >= bt.d[k + 1].tile_begin) ++k;
+    }
+    return k;
+}
+
+// Position of a wave in the launch: tile t of matrix k (packed byte `base`).
+struct Cursor {
+    uint32_t t, k, base;
+    bool valid;
+};
+
+template <int U, int MAXB>
+__device__ __forceinline__ Cursor cursor_at(const Batch<MAXB>& bt, uint32_t t, uint32_t k_hint) {
+    constexpr uint32_t kTileBytes = 256u * U;
+    Cursor c;
+    c.t = t;
+    c.valid = t < bt.total_tiles;
+    c.k = c.valid ? find_matrix(bt, t, k_hint) : k_hint;
+    // past the end: an offset beyond every buffer range (loads return 0, stores drop)
+    c.base = c.valid ? (t - bt.d[c.k].tile_begin) * kTileBytes : 0xFFFFF000u;
+    return c;
+}
+
+template <int DT, int MAXB>
+__device__ __forceinline__ void make_rsrcs(const Batch<MAXB>& bt, uint32_t k, __amdgpu_buffer_rsrc_t& rp,
+                                           __amdgpu_buffer_rsrc_t& ro) {
+    constexpr uint32_t kOB = out_bytes_per_packed_byte<DT>();
+    rp = __builtin_amdgcn_make_buffer_rsrc((void*)bt.d[k].packed, 0, bt.d[k].nbytes, kRsrcFlags);
+    ro = __builtin_amdgcn_make_buffer_rsrc((void*)bt.d[k].out, 0, bt.d[k].nbytes * kOB, kRsrcFlags);
+}
+
+// Persistent, software-pipelined flat kernel.  Each wave walks tiles
+// t, t + nwaves, ...; the loop is unrolled by two with the tiles in two
+// register sets (A, B) so that tile i+1's loads are in flight while tile i is
+// decoded and stored, with no register copies (a copy would force a wait on
+// the loads it copies).
+template <int DT, int MODE, int U, int AUXS, int AUXL, int MAXB>
+__global__ __launch_bounds__(kWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
+    __shared__ float lut[16];
+    if (threadIdx.x < 16) lut[threadIdx.x] = __uint_as_float(kNf4Bits[threadIdx.x]);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWg + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * kWavesPerWg;
+    if (t0 >= bt.total_tiles) return;
+
+    Cursor ca = cursor_at<U>(bt, t0, 0u);
+    __amdgpu_buffer_rsrc_t rpa, roa;
+    make_rsrcs<DT>(bt, ca.k, rpa, roa);
+    TileIn<U> A = tile_load<MODE, U, AUXL>(bt.d[ca.k], rpa, ca.base, lane);
+    // Out-of-range (dropped) stores with the loop body's count: loop entry then
+    // looks like the back edge to hipcc's waitcnt pass ([loads][stores]), so the
+    // in-loop waits count past the previous tile's stores instead of draining them.
+    {
+        constexpr int kStores = DT == NF4DQ_F32 ? 2 * U : U;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < kStores; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, roa, 0xFFFFF000u + 16u * j, 0, AUXS);
+    }
+    while (true) {
+        const Cursor cb = cursor_at<U>(bt, ca.t + nwaves, ca.k);
+        __amdgpu_buffer_rsrc_t rpb = rpa, rob = roa;
+        if (MAXB > 1 && cb.k != ca.k) make_rsrcs<DT>(bt, cb.k, rpb, rob);
+        const TileIn<U> B = tile_load<MODE, U, AUXL>(bt.d[cb.k], rpb, cb.base, lane);
+        tile_finish<DT, MODE, U, AUXS>(bt.d[ca.k], roa, lut, A, ca.base, lane);
+        if (!cb.valid) break;
+
+        const Cursor cn = cursor_at<U>(bt, cb.t + nwaves, cb.k);
+        __amdgpu_buffer_rsrc_t rpn = rpb, ron = rob;
+        if (MAXB > 1 && cn.k != cb.k) make_rsrcs<DT>(bt, cn.k, rpn, ron);
+        A = tile_load<MODE, U, AUXL>(bt.d[cn.k], rpn, cn.base, lane);
+        tile_finish<DT, MODE, U, AUXS>(bt.d[cb.k], rob, lut, B, cb.base, lane);
+        if (!cn.valid) break;
+        ca = cn;
+        rpa = rpn;
+        roa = ron;
+    }
+}
+
+// Any shape, reference / single-quant semantics: one thread per packed byte.
+struct RowsArgs {
+    const uint8_t* packed;
+    const uint8_t* a1;
+    const float* a2;
+    void* out;
+    int64_t m, n, stride, cols_b;  // cols_b = ceil(n/2) packed bytes used per row
+    int64_t nb, n2, bpr, groups, rs;
+};
+
+template <int DT, int MODE>
+__global__ __launch_bounds__(kWg) void nf4_rows_kernel(const RowsArgs A) {
+    __shared__ float lut[16];
+    if (threadIdx.x < 16) lut[threadIdx.x] = __uint_as_float(kNf4Bits[threadIdx.x]);
+    __syncthreads();
+    const int64_t total = A.m * A.cols_b;
+    for (int64_t i = (int64_t)blockIdx.x * kWg + threadIdx.x; i < total; i += (int64_t)gridDim.x * kWg) {
+        const int64_t r = i / A.cols_b;
+        const int64_t j = i - r * A.cols_b;
+        const int64_t b = j >> 5;
+        float s;
+        if constexpr (MODE == kRef) {
+            const float q = (float)A.a1[(r * A.bpr + b) % A.nb];
+            s = (q / 127.0f) * A.a2[(r * A.groups + (b >> 2)) % A.n2];
+        } else {
+            s = A.a2[r * A.rs + b];
+        }
+        const uint32_t byte = A.packed[r * A.stride + j];
+        const int64_t c = 2 * j;
+        store1<DT>(A.out, r * A.n + c, lut[byte >> 4] * s);
+        if (c + 1 < A.n) store1<DT>(A.out, r * A.n + c + 1, lut[byte & 15u] * s);
+    }
+}
+
+// Any length, bitsandbytes semantics: one thread per packed byte.
+struct BnbBytesArgs {
+    const uint8_t* packed;
+    const uint8_t* a1;
+    const float* code2;
+    const float* a2;
+    void* out;
+    float offset;
+    int64_t numel;
+    int32_t blk_shift_elems, blk2_shift;
+    int32_t single;
+};
+
+template <int DT>
+__global__ __launch_bounds__(kWg) void nf4_bnb_bytes_kernel(const BnbBytesArgs A) {
+    __shared__ float lut[16];
+    if (threadIdx.x < 16) lut[threadIdx.x] = __uint_as_float(kNf4Bits[threadIdx.x]);
+    __syncthreads();
+    const int64_t nbytes = (A.numel + 1) / 2;
+    for (int64_t i = (int64_t)blockIdx.x * kWg + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * kWg) {
+        const int64_t e = 2 * i;
+        const int64_t blk = e >> A.blk_shift_elems;
+        const float s = A.single ? A.a2[blk] : A.code2[A.a1[blk]] * A.a2[blk >> A.blk2_shift] + A.offset;
+        const uint32_t byte = A.packed[i];
+        store1<DT>(A.out, e, lut[byte >> 4] * s);
+        if (e + 1 < A.numel) store1<DT>(A.out, e + 1, lut[byte & 15u] * s);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+inline int hip_rc(hipError_t e) { return e == hipSuccess ? NF4DQ_OK : NF4DQ_ERR_HIP_BASE + (int)e; }
+
+inline bool valid_dtype(int32_t d) { return d == NF4DQ_F16 || d == NF4DQ_BF16 || d == NF4DQ_F32; }
+
+inline bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+inline int ilog2(uint64_t v) {
+    int s = 0;
+    while ((uint64_t(1) << s) < v) ++s;
+    return s;
+}
+
+constexpr nf4_launch_cfg kDefaultCfg = {8, 0, 1, 0};
+
+int cu_count() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 256;
+    return cus;
+}
+
+template <int MAXB>
+int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_launch_cfg& cfg, hipStream_t st) {
+    if (bt.total_tiles == 0) return NF4DQ_OK;
+    const uint32_t U = cfg.tile_dwords == 8 ? 8u : 4u;
+    // total_tiles was counted with 1 KiB tiles; a 2 KiB tile covers two of them.
+    Batch<MAXB> b = bt;
+    if (U == 8) {
+        uint32_t acc = 0;
+        for (uint32_t i = 0; i < b.count; ++i) {
+            b.d[i].tile_begin = acc;
+            acc += (b.d[i].nbytes + 2047u) / 2048u;
+        }
+        b.total_tiles = acc;
+    }
+    uint64_t blocks = (b.total_tiles + kWavesPerWg - 1) / kWavesPerWg;
+    if (cfg.blocks_per_cu > 0) {
+        const uint64_t cap = (uint64_t)cfg.blocks_per_cu * (uint64_t)cu_count();
+        if (blocks > cap) blocks = cap;
+    }
+    const dim3 grid((unsigned)blocks), block(kWg);
+    const int auxs = cfg.nontemporal ? kAuxNt : 0;
+    const int auxl = (cfg.flags & NF4DQ_CFG_NT_LOADS) ? kAuxNt : 0;
+
+#define NF4_LAUNCH(DT_, MODE_, U_, AS_, AL_) \
+    hipLaunchKernelGGL((nf4_flat_kernel<DT_, MODE_, U_, AS_, AL_, MAXB>), grid, block, 0, st, b)
+#define NF4_DISPATCH_AUX(DT_, MODE_, U_)                       \
+    do {                                                       \
+        if (auxs && auxl) NF4_LAUNCH(DT_, MODE_, U_, kAuxNt, kAuxNt); \
+        else if (auxs) NF4_LAUNCH(DT_, MODE_, U_, kAuxNt, 0);  \
+        else if (auxl) NF4_LAUNCH(DT_, MODE_, U_, 0, kAuxNt);  \
+        else NF4_LAUNCH(DT_, MODE_, U_, 0, 0);                 \
+    } while (0)
+#define NF4_DISPATCH_U(DT_, MODE_)                                 \
+    do {                                                           \
+        if (U == 8) NF4_DISPATCH_AUX(DT_, MODE_, 8);               \
+        else NF4_DISPATCH_AUX(DT_, MODE_, 4);                      \
+    } while (0)
+#define NF4_DISPATCH_MODE(DT_)                                    \
+    do {                                                          \
+        switch (mode) {                                           \
+            case kRef: NF4_DISPATCH_U(DT_, kRef); break;          \
+            case kSingle: NF4_DISPATCH_U(DT_, kSingle); break;    \
+            case kBnb: NF4_DISPATCH_U(DT_, kBnb); break;          \
+            default: NF4_DISPATCH_U(DT_, kBnbSingle); break;      \
+        }                                                         \
+    } while (0)
+
+    if (dtype == NF4DQ_BF16) NF4_DISPATCH_MODE(NF4DQ_BF16);
+    else if (dtype == NF4DQ_F16) NF4_DISPATCH_MODE(NF4DQ_F16);
+    else NF4_DISPATCH_MODE(NF4DQ_F32);
+#undef NF4_DISPATCH_MODE
+#undef NF4_DISPATCH_U
+#undef NF4_DISPATCH_AUX
+#undef NF4_LAUNCH
+    return hip_rc(hipGetLastError());
+}
+
+inline unsigned rows_grid(int64_t work) {
+    int64_t b = (work + kWg - 1) / kWg;
+    if (b > 65536) b = 65536;  // grid-stride beyond this
+    if (b < 1) b = 1;
+    return (unsigned)b;
+}
+
+// Validation shared by the reference-semantics entry points (mirrors what the
+// reference's .view(m, -1) and slicing accept, kernel_optimized.py:229, :288-312).
+int check_common(const uint8_t* packed, int64_t packed_len, const void* out, int32_t dtype, int64_t m, int64_t n) {
+    if (!valid_dtype(dtype)) return NF4DQ_ERR_ARG;
+    if (m < 0 || n < 0 || packed_len < 0) return NF4DQ_ERR_ARG;
+    if (m == 0 || n == 0) return NF4DQ_OK;
+    if (!packed || !out) return NF4DQ_ERR_ARG;
+    if (packed_len % m) return NF4DQ_ERR_SHAPE;
+    if (packed_len / m < (n + 1) / 2) return NF4DQ_ERR_SHAPE;
+    return NF4DQ_OK;
+}
+
+// Fill a flat-path descriptor for reference / single semantics, or return false
+// when the matrix needs the rows kernel.
+bool flat_eligible(const uint8_t* packed, int64_t packed_len, const void* out, int64_t m, int64_t n) {
+    // buffer descriptors address <= 4 GiB of output: keep packed bytes < 2^29
+    return n % 64 == 0 && packed_len == m * (n / 2) && packed_len < (int64_t(1) << 29) &&
+           aligned(packed, 4) && aligned(out, 16);
+}
+
+Desc ref_desc(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int64_t nb, const float* a2,
+              int64_t n2, void* out, int64_t n) {
+    Desc d{};
+    d.packed = reinterpret_cast<const uint32_t*>(packed);
+    d.a1 = a1;
+    d.a2 = a2;
+    d.out = reinterpret_cast<u32x4*>(out);
+    d.nbytes = (uint32_t)packed_len;
+    const int64_t bpr = (n + 63) / 64;
+    d.groups = (uint32_t)((bpr + 3) / 4);
+    // moduli above 2^31 never wrap for indices < 2^31: clamp keeps FastDiv valid
+    d.nb = make_fastdiv((uint32_t)(nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : nb));
+    d.n2 = make_fastdiv((uint32_t)(n2 > (int64_t(1) << 31) ? (int64_t(1) << 31) : n2));
+    d.bpr = make_fastdiv((uint32_t)bpr);
+    d.blk_shift = 5;  // 64 elements = 32 packed bytes
+    return d;
+}
+
+int ref_impl(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int64_t nb, const float* a2, int64_t n2,
+             void* out, int32_t dtype, int64_t m, int64_t n, const nf4_launch_cfg& cfg, hipStream_t st) {
+    int rc = check_common(packed, packed_len, out, dtype, m, n);
+    if (rc || m == 0 || n == 0) return rc;
+    if (!a1 || !a2 || nb <= 0 || n2 <= 0) return NF4DQ_ERR_ARG;
+    if (flat_eligible(packed, packed_len, out, m, n)) {
+        Batch<1> b{};
+        b.d[0] = ref_desc(packed, packed_len, a1, nb, a2, n2, out, n);
+        b.count = 1;
+        b.total_tiles = (uint32_t)((packed_len + 1023) / 1024);
+        return launch_flat_batch(b, dtype, kRef, cfg, st);
+    }
+    RowsArgs A{};
+    A.packed = packed;
+    A.a1 = a1;
+    A.a2 = a2;
+    A.out = out;
+    A.m = m;
+    A.n = n;
+    A.stride = packed_len / m;
+    A.cols_b = (n + 1) / 2;
+    A.nb = nb;
+    A.n2 = n2;
+    A.bpr = (n + 63) / 64;
+    A.groups = (A.bpr + 3) / 4;
+    const unsigned g = rows_grid(m * A.cols_b);
+    if (dtype == NF4DQ_BF16) hipLaunchKernelGGL((nf4_rows_kernel<NF4DQ_BF16, kRef>), dim3(g), dim3(kWg), 0, st, A);
+    else if (dtype == NF4DQ_F16) hipLaunchKernelGGL((nf4_rows_kernel<NF4DQ_F16, kRef>), dim3(g), dim3(kWg), 0, st, A);
+    else hipLaunchKernelGGL((nf4_rows_kernel<NF4DQ_F32, kRef>), dim3(g), dim3(kWg), 0, st, A);
+    return hip_rc(hipGetLastError());
+}
+
+}  // namespace
+
+extern "C" {
+
+int nf4_dequant_ref(const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q, int64_t nb,
+                    const float* absmax2, int64_t n2, void* out, int32_t out_dtype, int64_t m, int64_t n,
+                    void* hip_stream) {
+    return ref_impl(packed, packed_len, absmax_q, nb, absmax2, n2, out, out_dtype, m, n, kDefaultCfg,
+                    reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q, int64_t nb,
+                        const float* absmax2, int64_t n2, void* out, int32_t out_dtype, int64_t m, int64_t n,
+                        const nf4_launch_cfg* cfg, void* hip_stream) {
+    nf4_launch_cfg c = cfg ? *cfg : kDefaultCfg;
+    if (c.tile_dwords != 4 && c.tile_dwords != 8) return NF4DQ_ERR_ARG;
+    if (c.flags & ~NF4DQ_CFG_NT_LOADS) return NF4DQ_ERR_ARG;
+    return ref_impl(packed, packed_len, absmax_q, nb, absmax2, n2, out, out_dtype, m, n, c,
+                    reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+int nf4_dequant_single(const uint8_t* packed, int64_t packed_len, const float* absmax, int64_t absmax_len,
+                       void* out, int32_t out_dtype, int64_t m, int64_t n, void* hip_stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    int rc = check_common(packed, packed_len, out, out_dtype, m, n);
+    if (rc || m == 0 || n == 0) return rc;
+    if (!absmax || absmax_len < 0) return NF4DQ_ERR_ARG;
+    const int64_t bpr = (n + 63) / 64;
+    if (absmax_len % m || absmax_len / m < bpr) return NF4DQ_ERR_SHAPE;
+    const int64_t rs = absmax_len / m;
+    if (flat_eligible(packed, packed_len, out, m, n) && absmax_len < (int64_t(1) << 31)) {
+        Batch<1> b{};
+        b.d[0] = ref_desc(packed, packed_len, nullptr, 1, absmax, 1, out, n);
+        b.d[0].n2 = make_fastdiv((uint32_t)rs);
+        b.count = 1;
+        b.total_tiles = (uint32_t)((packed_len + 1023) / 1024);
+        return launch_flat_batch(b, out_dtype, kSingle, kDefaultCfg, st);
+    }
+    RowsArgs A{};
+    A.packed = packed;
+    A.a2 = absmax;
+    A.out = out;
+    A.m = m;
+    A.n = n;
+    A.stride = packed_len / m;
+    A.cols_b = (n + 1) / 2;
+    A.bpr = bpr;
+    A.rs = rs;
+    const unsigned g = rows_grid(m * A.cols_b);
+    if (out_dtype == NF4DQ_BF16) hipLaunchKernelGGL((nf4_rows_kernel<NF4DQ_BF16, kSingle>), dim3(g), dim3(kWg), 0, st, A);
+    else if (out_dtype == NF4DQ_F16) hipLaunchKernelGGL((nf4_rows_kernel<NF4DQ_F16, kSingle>), dim3(g), dim3(kWg), 0, st, A);
+    else hipLaunchKernelGGL((nf4_rows_kernel<NF4DQ_F32, kSingle>), dim3(g), dim3(kWg), 0, st, A);
+    return hip_rc(hipGetLastError());
+}
+
+int nf4_dequant_ref_batched(const nf4_matrix_desc* descs, int32_t count, int32_t out_dtype, void* hip_stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    if (count < 0 || (count > 0 && !descs)) return NF4DQ_ERR_ARG;
+    if (!valid_dtype(out_dtype)) return NF4DQ_ERR_ARG;
+    // Validate everything before launching anything.
+    for (int32_t i = 0; i < count; ++i) {
+        const nf4_matrix_desc& d = descs[i];
+        int rc = check_common(d.packed, d.packed_len, d.out, out_dtype, d.m, d.n);
+        if (rc) return rc;
+        if (d.m == 0 || d.n == 0) continue;
+        if (!d.absmax_q || !d.absmax2 || d.nb <= 0 || d.n2 <= 0) return NF4DQ_ERR_ARG;
+    }
+    Batch<NF4DQ_BATCH_MAX> b{};
+    b.count = 0;
+    b.total_tiles = 0;
+    for (int32_t i = 0; i < count; ++i) {
+        const nf4_matrix_desc& d = descs[i];
+        if (d.m == 0 || d.n == 0) continue;
+        if (!flat_eligible(d.packed, d.packed_len, d.out, d.m, d.n)) {
+            int rc = ref_impl(d.packed, d.packed_len, d.absmax_q, d.nb, d.absmax2, d.n2, d.out, out_dtype, d.m, d.n,
+                              kDefaultCfg, st);
+            if (rc) return rc;
+            continue;
+        }
+        Desc x = ref_desc(d.packed, d.packed_len, d.absmax_q, d.nb, d.absmax2, d.n2, d.out, d.n);
+        x.tile_begin = b.total_tiles;
+        b.d[b.count++] = x;
+        b.total_tiles += (uint32_t)((d.packed_len + 1023) / 1024);
+        if (b.count == NF4DQ_BATCH_MAX || b.total_tiles > (1u << 30)) {
+            int rc = launch_flat_batch(b, out_dtype, kRef, kDefaultCfg, st);
+            if (rc) return rc;
+            b.count = 0;
+            b.total_tiles = 0;
+        }
+    }
+    if (b.count) return launch_flat_batch(b, out_dtype, kRef, kDefaultCfg, st);
+    return NF4DQ_OK;
+}
+
+static int bnb_common(const uint8_t* packed, const uint8_t* a1, int64_t nb, const float* code2, const float* a2,
+                      int64_t n2, float offset, void* out, int32_t dtype, int64_t numel, int32_t blocksize,
+                      int32_t blocksize2, bool single, hipStream_t st) {
+    if (!valid_dtype(dtype)) return NF4DQ_ERR_ARG;
+    if (numel < 0) return NF4DQ_ERR_ARG;
+    if (numel == 0) return NF4DQ_OK;
+    if (!packed || !out || !a2) return NF4DQ_ERR_ARG;
+    if (blocksize < 64 || (blocksize & (blocksize - 1))) return NF4DQ_ERR_ARG;
+    const int64_t nblk = (numel + blocksize - 1) / blocksize;
+    if (nb < nblk) return NF4DQ_ERR_SHAPE;
+    if (!single) {
+        if (!a1 || !code2) return NF4DQ_ERR_ARG;
+        if (blocksize2 <= 0 || (blocksize2 & (blocksize2 - 1))) return NF4DQ_ERR_ARG;
+        if (n2 < (nblk + blocksize2 - 1) / blocksize2) return NF4DQ_ERR_SHAPE;
+    }
+    const int mode = single ? kBnbSingle : kBnb;
+    if (numel % 8 == 0 && numel / 2 < (int64_t(1) << 29) && aligned(packed, 4) && aligned(out, 16)) {
+        Batch<1> b{};
+        Desc& d = b.d[0];
+        d.packed = reinterpret_cast<const uint32_t*>(packed);
+        d.a1 = a1;
+        d.a2 = a2;
+        d.code2 = code2;
+        d.out = reinterpret_cast<u32x4*>(out);
+        d.offset = offset;
+        d.nbytes = (uint32_t)(numel / 2);
+        d.blk_shift = (uint32_t)ilog2((uint64_t)blocksize / 2);
+        d.blk2_shift = single ? 0u : (uint32_t)ilog2((uint64_t)blocksize2);
+        b.count = 1;
+        b.total_tiles = (d.nbytes + 1023u) / 1024u;
+        return launch_flat_batch(b, dtype, mode, kDefaultCfg, st);
+    }
+    BnbBytesArgs A{};
+    A.packed = packed;
+    A.a1 = a1;
+    A.code2 = code2;
+    A.a2 = a2;
+    A.out = out;
+    A.offset = offset;
+    A.numel = numel;
+    A.blk_shift_elems = ilog2((uint64_t)blocksize);
+    A.blk2_shift = single ? 0 : ilog2((uint64_t)blocksize2);
+    A.single = single ? 1 : 0;
+    const unsigned g = rows_grid((numel + 1) / 2);
+    if (dtype == NF4DQ_BF16) hipLaunchKernelGGL((nf4_bnb_bytes_kernel<NF4DQ_BF16>), dim3(g), dim3(kWg), 0, st, A);
+    else if (dtype == NF4DQ_F16) hipLaunchKernelGGL((nf4_bnb_bytes_kernel<NF4DQ_F16>), dim3(g), dim3(kWg), 0, st, A);
+    else hipLaunchKernelGGL((nf4_bnb_bytes_kernel<NF4DQ_F32>), dim3(g), dim3(kWg), 0, st, A);
+    return hip_rc(hipGetLastError());
+}
+
+int nf4_dequant_bnb(const uint8_t* packed, const uint8_t* absmax_q, int64_t nb, const float* code2,
+                    const float* absmax2, int64_t n2, float offset, void* out, int32_t out_dtype, int64_t numel,
+                    int32_t blocksize, int32_t blocksize2, void* hip_stream) {
+    return bnb_common(packed, absmax_q, nb, code2, absmax2, n2, offset, out, out_dtype, numel, blocksize, blocksize2,
+                      false, reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+int nf4_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t nabs, void* out, int32_t out_dtype,
+                           int64_t numel, int32_t blocksize, void* hip_stream) {
+    return bnb_common(packed, nullptr, nabs, nullptr, absmax, 0, 0.0f, out, out_dtype, numel, blocksize, 1, true,
+                      reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+const char* nf4_strerror(int code) {
+    switch (code) {
+        case NF4DQ_OK: return "ok";
+        case NF4DQ_ERR_ARG: return "invalid argument (null pointer, dtype or negative size)";
+        case NF4DQ_ERR_SHAPE: return "shape mismatch (packed weight / absmax cannot be viewed as the reference does)";
+        case NF4DQ_ERR_TOO_LARGE: return "matrix too large for one launch";
+        default: break;
+    }
+    if (code >= NF4DQ_ERR_HIP_BASE) return hipGetErrorString((hipError_t)(code - NF4DQ_ERR_HIP_BASE));
+    return "unknown error";
+}
+
+const char* nf4_version(void) { return "nf4dq 0.1.0 gfx950"; }
+
+}  // extern "C"

@@ -1,0 +1,217 @@
+"""Drop-in host side of the NF4 dequantization path (MI355X / gfx950).
+
+Mirrors the reference's operator interface
+(/root/reference/nf4_triton_dequantization/kernel_optimized.py):
+
+* ``triton_dequantize_nf4(module)``          <- :113-139 (+ launcher :142-205)
+* ``reset_triton_dequantize_state()``       <- :317-319 (no-op; no caches here either)
+
+Same attribute reads (``module.weight.data``, ``.weight.quant_state.absmax``,
+``.quant_state.state2.absmax``, ``.quant_state.dtype``, ``module.out_features``,
+``module.in_features``), same value casts (qweight -> uint8 :162-163, nested
+absmax -> fp32 :182), same output (new row-major ``[m, n]`` tensor of
+``quant_state.dtype`` on the weight's device, :189), launched on the caller's
+current stream.  A uint8 absmax takes the double-dequant kernel; any other
+absmax dtype takes the single-quant kernel, exactly where the reference falls
+back to ``_aggressive_pytorch_t4`` (:166-167 -> :273-274).
+
+Error behaviour: the reference raises from torch/Triton (RuntimeError for a
+tensor it cannot view or a CPU tensor -- "0 active drivers" --,
+AttributeError for a missing ``state2``, ZeroDivisionError for an empty
+absmax); the same exception types are raised here.  There is no CPU path and
+no silent fallback: compute always goes through ``libnf4dq.so``.
+
+Extensions beyond the reference: ``dequantize_nf4_many`` (one
+launch for many weights), ``dequantize_nf4_bnb`` (bitsandbytes semantics,
+parity unpinned) and ``dequantize_nf4_into`` (caller-provided output).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, List, Optional
+
+import torch
+
+from . import _lib
+
+_DTYPE_CODE = {torch.float16: _lib.F16, torch.bfloat16: _lib.BF16, torch.float32: _lib.F32}
+
+
+def _dtype_code(dtype: torch.dtype) -> int:
+    try:
+        return _DTYPE_CODE[dtype]
+    except KeyError:
+        raise TypeError(f"unsupported quant_state.dtype {dtype}; expected float16, bfloat16 or float32") from None
+
+
+def _require_device(t: torch.Tensor) -> None:
+    if t.device.type != "cuda":
+        # The reference hands a CPU tensor to Triton, which raises
+        # RuntimeError("0 active drivers ..."); there is no CPU path here either.
+        raise RuntimeError(
+            f"triton_dequantize_nf4: weight is on '{t.device}'; the NF4 HIP path needs a ROCm device tensor")
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _as_u8_flat(q: torch.Tensor) -> torch.Tensor:
+    if q.dtype != torch.uint8:
+        q = q.to(torch.uint8)              # value cast, as :162-163
+    return q.contiguous().view(-1)
+
+
+def _prepare(module):
+    """Attribute reads and casts of kernel_optimized.py:146-186."""
+    weight = module.weight
+    quant_state = weight.quant_state
+    qweight = weight.data
+    absmax = quant_state.absmax
+    absmax32 = quant_state.state2.absmax    # AttributeError when state2 is None, as :151
+    dtype = quant_state.dtype
+    m = int(module.out_features)
+    n = int(module.in_features)
+    return qweight, absmax, absmax32, dtype, m, n
+
+
+def dequantize_nf4_into(qweight: torch.Tensor, absmax: torch.Tensor, absmax32: torch.Tensor,
+                        out: torch.Tensor, m: int, n: int) -> torch.Tensor:
+    """Dequantize into a caller-provided contiguous ``out`` ([m, n] elements, fp16/bf16/fp32)."""
+    _require_device(qweight)
+    code = _dtype_code(out.dtype)
+    if not out.is_contiguous() or out.numel() != m * n:
+        raise RuntimeError("dequantize_nf4_into: out must be a contiguous tensor of m*n elements")
+    if m == 0 or n == 0:
+        return out
+    q = _as_u8_flat(qweight)
+    L = _lib.lib()
+    stream = _stream_ptr(q.device)
+    if absmax.dtype == torch.uint8:
+        a1 = absmax.contiguous().view(-1)
+        a2 = absmax32.reshape(-1)
+        if a2.dtype != torch.float32:
+            a2 = a2.to(torch.float32)      # :182
+        a2 = a2.contiguous()
+        if a1.numel() == 0 or a2.numel() == 0:
+            # reference: repeats = ceil(total / 0) -> ZeroDivisionError (:175, :184)
+            raise ZeroDivisionError("integer division or modulo by zero (empty absmax)")
+        rc = L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                               out.data_ptr(), code, m, n, stream)
+    else:
+        # single-quant branch (:166-167 -> :273-274): absmax.view(m, -1)[:, :bpr].to(float32)
+        am = absmax.reshape(-1)
+        if am.dtype != torch.float32:
+            am = am.to(torch.float32)
+        am = am.contiguous()
+        rc = L.nf4_dequant_single(q.data_ptr(), q.numel(), am.data_ptr(), am.numel(), out.data_ptr(), code,
+                                  m, n, stream)
+    _lib.check(rc, "nf4 dequantize")
+    return out
+
+
+def triton_dequantize_nf4(module) -> torch.Tensor:
+    """Dequantize a bitsandbytes-layout NF4 ``Linear4bit`` weight to ``[out_features, in_features]``.
+
+    Drop-in for ``nf4_triton_dequantization.triton_dequantize_nf4``
+    (kernel_optimized.py:113).  Returns a new contiguous tensor of
+    ``quant_state.dtype`` on the weight's device.
+    """
+    qweight, absmax, absmax32, dtype, m, n = _prepare(module)
+    _require_device(qweight)
+    code_ok = _dtype_code(dtype)  # noqa: F841  -- raise before allocating
+    out = torch.empty((m, n), dtype=dtype, device=qweight.device)
+    if qweight.device.index is not None and qweight.device.index != torch.cuda.current_device():
+        with torch.cuda.device(qweight.device):
+            return dequantize_nf4_into(qweight, absmax, absmax32, out, m, n)
+    return dequantize_nf4_into(qweight, absmax, absmax32, out, m, n)
+
+
+def reset_triton_dequantize_state() -> None:
+    """No-op, as kernel_optimized.py:317-319: the path keeps no cached state."""
+    return None
+
+
+def dequantize_nf4_many(modules: Iterable) -> List[torch.Tensor]:
+    """Dequantize several weights with as few launches as possible.
+
+    Equivalent to ``[triton_dequantize_nf4(m) for m in modules]`` (the
+    benchmark.py:68-84 pattern) but folds every uint8-absmax weight of one
+    device and dtype into batched launches of up to ``NF4DQ_BATCH_MAX`` matrices.
+    """
+    modules = list(modules)
+    outs: List[Optional[torch.Tensor]] = [None] * len(modules)
+    groups = {}
+    keep = []  # tensors referenced by descriptors must outlive the launch
+    for i, mod in enumerate(modules):
+        qweight, absmax, absmax32, dtype, m, n = _prepare(mod)
+        _require_device(qweight)
+        if absmax.dtype != torch.uint8:
+            outs[i] = triton_dequantize_nf4(mod)
+            continue
+        code = _dtype_code(dtype)
+        out = torch.empty((m, n), dtype=dtype, device=qweight.device)
+        outs[i] = out
+        if m == 0 or n == 0:
+            continue
+        q = _as_u8_flat(qweight)
+        a1 = absmax.contiguous().view(-1)
+        a2 = absmax32.reshape(-1)
+        a2 = (a2 if a2.dtype == torch.float32 else a2.to(torch.float32)).contiguous()
+        if a1.numel() == 0 or a2.numel() == 0:
+            raise ZeroDivisionError("integer division or modulo by zero (empty absmax)")
+        keep.extend((q, a1, a2))
+        d = _lib.MatrixDesc(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                            out.data_ptr(), m, n)
+        groups.setdefault((q.device, code), []).append(d)
+    L = _lib.lib()
+    for (device, code), descs in groups.items():
+        arr = (_lib.MatrixDesc * len(descs))(*descs)
+        with torch.cuda.device(device):
+            rc = L.nf4_dequant_ref_batched(arr, len(descs), code, _stream_ptr(device))
+        _lib.check(rc, "nf4 batched dequantize")
+    if keep:
+        # the launches read q/a1/a2 asynchronously: tie their lifetime to the stream
+        for t in keep:
+            t.record_stream(torch.cuda.current_stream(t.device))
+    return outs  # type: ignore[return-value]
+
+
+def dequantize_nf4_bnb(module) -> torch.Tensor:
+    """bitsandbytes ``dequantize_4bit`` semantics (parity unpinned).
+
+    Reads ``quant_state.{absmax, code?, offset, blocksize, shape, dtype}`` and, when
+    nested, ``state2.{absmax, code, blocksize}``; output has ``quant_state.shape``.
+    """
+    weight = module.weight
+    qs = weight.quant_state
+    _require_device(weight.data)
+    q = _as_u8_flat(weight.data)
+    shape = tuple(qs.shape) if getattr(qs, "shape", None) is not None else (int(module.out_features),
+                                                                            int(module.in_features))
+    numel = 1
+    for s in shape:
+        numel *= int(s)
+    code = _dtype_code(qs.dtype)
+    out = torch.empty(shape, dtype=qs.dtype, device=q.device)
+    if numel == 0:
+        return out
+    bs = int(qs.blocksize)
+    L = _lib.lib()
+    stream = _stream_ptr(q.device)
+    nested = getattr(qs, "state2", None) is not None and qs.absmax.dtype == torch.uint8
+    if nested:
+        a1 = qs.absmax.contiguous().view(-1)
+        code2 = qs.state2.code.to(torch.float32).contiguous()
+        a2 = qs.state2.absmax.to(torch.float32).contiguous().view(-1)
+        off = qs.offset
+        off = float(off.item()) if torch.is_tensor(off) else float(off or 0.0)
+        rc = L.nf4_dequant_bnb(q.data_ptr(), a1.data_ptr(), a1.numel(), code2.data_ptr(), a2.data_ptr(),
+                               a2.numel(), ctypes.c_float(off), out.data_ptr(), code, numel, bs,
+                               int(qs.state2.blocksize), stream)
+    else:
+        am = qs.absmax.to(torch.float32).contiguous().view(-1)
+        rc = L.nf4_dequant_bnb_single(q.data_ptr(), am.data_ptr(), am.numel(), out.data_ptr(), code, numel,
+                                      bs, stream)
+    _lib.check(rc, "nf4 bnb dequantize")
+    return out

@@ -1,0 +1,114 @@
+"""C-ABI library: loads, exports every symbol include/nf4_dequant.h declares, and
+rejects bad arguments on the host before any device work (no GPU needed)."""
+import ctypes
+import re
+
+import pytest
+
+from nf4_triton_dequantization_amd import _lib
+
+
+def _header_functions():
+    text = open(_lib.HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(nf4_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = _header_functions()
+    for name in ("nf4_dequant_ref", "nf4_dequant_single", "nf4_dequant_ref_batched", "nf4_dequant_bnb",
+                 "nf4_dequant_bnb_single", "nf4_dequant_ref_cfg", "nf4_strerror", "nf4_version"):
+        assert name in fns
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    for name in _header_functions():
+        assert hasattr(L, name), name
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
+
+
+def test_header_constants_match_binding():
+    text = open(_lib.HEADER_PATH).read()
+    consts = dict(re.findall(r"#define\s+(NF4DQ_\w+)\s+(\d+)", text))
+    assert int(consts["NF4DQ_F16"]) == _lib.F16
+    assert int(consts["NF4DQ_BF16"]) == _lib.BF16
+    assert int(consts["NF4DQ_F32"]) == _lib.F32
+    assert int(consts["NF4DQ_ERR_ARG"]) == _lib.ERR_ARG
+    assert int(consts["NF4DQ_ERR_SHAPE"]) == _lib.ERR_SHAPE
+    assert int(consts["NF4DQ_BATCH_MAX"]) == _lib.BATCH_MAX
+
+
+def test_struct_layouts():
+    assert ctypes.sizeof(_lib.MatrixDesc) == 9 * 8
+    assert ctypes.sizeof(_lib.LaunchCfg) == 16
+
+
+def test_version_and_strerror():
+    L = _lib.lib()
+    assert b"gfx950" in L.nf4_version()
+    assert L.nf4_strerror(0) == b"ok"
+    assert b"shape" in L.nf4_strerror(2)
+
+
+FAKE = 0x1000  # never dereferenced: every call below fails validation first
+
+
+@pytest.mark.parametrize("args,want", [
+    # bad dtype
+    ((FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 7, 2, 64, None), _lib.ERR_ARG),
+    # negative m
+    ((FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 0, -1, 64, None), _lib.ERR_ARG),
+    # packed_len not divisible by m (view(m, -1) fails, kernel_optimized.py:229)
+    ((FAKE, 65, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, None), _lib.ERR_SHAPE),
+    # packed rows shorter than ceil(n/2)
+    ((FAKE, 60, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, None), _lib.ERR_SHAPE),
+    # empty absmax
+    ((FAKE, 64, FAKE, 0, FAKE, 1, FAKE, 1, 2, 64, None), _lib.ERR_ARG),
+    # null output
+    ((FAKE, 64, FAKE, 2, FAKE, 1, None, 1, 2, 64, None), _lib.ERR_ARG),
+    # empty matrix: nothing to do, nothing launched
+    ((None, 0, None, 0, None, 0, None, 1, 0, 64, None), _lib.OK),
+    ((None, 0, None, 0, None, 0, None, 1, 5, 0, None), _lib.OK),
+])
+def test_ref_validation(args, want):
+    assert _lib.lib().nf4_dequant_ref(*args) == want
+
+
+def test_single_validation():
+    L = _lib.lib()
+    # absmax cannot be viewed as (m, -1)
+    assert L.nf4_dequant_single(FAKE, 64, FAKE, 3, FAKE, 1, 2, 64, None) == _lib.ERR_SHAPE
+    # absmax rows shorter than blocks per row
+    assert L.nf4_dequant_single(FAKE, 128, FAKE, 2, FAKE, 1, 2, 128, None) == _lib.ERR_SHAPE
+
+
+def test_bnb_validation():
+    L = _lib.lib()
+    # blocksize not a power of two / below 64
+    assert L.nf4_dequant_bnb(FAKE, FAKE, 4, FAKE, FAKE, 1, 0.0, FAKE, 1, 256, 96, 256, None) == _lib.ERR_ARG
+    assert L.nf4_dequant_bnb(FAKE, FAKE, 8, FAKE, FAKE, 1, 0.0, FAKE, 1, 256, 32, 256, None) == _lib.ERR_ARG
+    # too few absmax blocks
+    assert L.nf4_dequant_bnb(FAKE, FAKE, 3, FAKE, FAKE, 1, 0.0, FAKE, 1, 256, 64, 256, None) == _lib.ERR_SHAPE
+    # too few nested absmax
+    assert L.nf4_dequant_bnb(FAKE, FAKE, 600, FAKE, FAKE, 2, 0.0, FAKE, 1, 600 * 64, 64, 256, None) == _lib.ERR_SHAPE
+    assert L.nf4_dequant_bnb_single(FAKE, FAKE, 3, FAKE, 1, 256, 64, None) == _lib.ERR_SHAPE
+    assert L.nf4_dequant_bnb_single(None, None, 0, None, 1, 0, 64, None) == _lib.OK
+
+
+def test_batched_validation():
+    L = _lib.lib()
+    d = (_lib.MatrixDesc * 2)(_lib.MatrixDesc(FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 2, 64),
+                              _lib.MatrixDesc(FAKE, 65, FAKE, 2, FAKE, 1, FAKE, 2, 64))
+    # the second descriptor is invalid: nothing is launched, the error is reported
+    assert L.nf4_dequant_ref_batched(d, 2, 1, None) == _lib.ERR_SHAPE
+    assert L.nf4_dequant_ref_batched(d, 1, 9, None) == _lib.ERR_ARG
+    assert L.nf4_dequant_ref_batched(None, 0, 1, None) == _lib.OK
+
+
+def test_cfg_validation():
+    L = _lib.lib()
+    cfg = _lib.LaunchCfg(3, 0, 0, 0)
+    assert L.nf4_dequant_ref_cfg(FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, ctypes.byref(cfg), None) == _lib.ERR_ARG
+    cfg = _lib.LaunchCfg(4, 0, 0, 8)
+    assert L.nf4_dequant_ref_cfg(FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, ctypes.byref(cfg), None) == _lib.ERR_ARG
