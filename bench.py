@@ -111,7 +111,7 @@ def main():
     ap.add_argument("--sets", type=int, default=16, help="rotating buffer sets (>256 MiB total)")
     ap.add_argument("--streams", type=int, default=1, help="streams the steps round-robin over")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--tile-dwords", type=int, default=8)
+    ap.add_argument("--tile-dwords", type=int, default=4)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=1)
     ap.add_argument("--flags", type=int, default=0, help="NF4DQ_CFG_* bits (1 = nt loads)")

@@ -99,6 +99,10 @@ int nf4_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t n
  * per CU (0 = one workgroup per 4 tiles, no cap); nontemporal: 0/1 streaming
  * (nt) output stores; flags: NF4DQ_CFG_* bits. */
 #define NF4DQ_CFG_NT_LOADS 1   /* nt cache policy on the packed-weight loads */
+/* bits 8..11: log2 of the number of contiguous tile segments (0..6); block b
+ * works in segment b % 2^k (k = 3: one segment per XCD under round-robin placement) */
+#define NF4DQ_CFG_SEG_SHIFT_BIT 8
+#define NF4DQ_CFG_SEG_SHIFT_MASK 0xF00
 typedef struct nf4_launch_cfg {
     int32_t tile_dwords;
     int32_t blocks_per_cu;

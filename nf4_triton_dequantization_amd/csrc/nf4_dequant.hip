@@ -37,14 +37,6 @@
 
 namespace {
 
-// NF4 code points as the fp32 bit patterns of kernel_optimized.py:234-239.
-__constant__ uint32_t kNf4Bits[16] = {
-    0xbf800000u, 0xbf3239b1u, 0xbf066b30u, 0xbeca32a0u,
-    0xbe91a24du, 0xbe3d353fu, 0xbdba7871u, 0x00000000u,
-    0x3da2faffu, 0x3e24cae3u, 0x3e7c04ddu, 0x3ead033au,
-    0x3ee1a4b8u, 0x3f1007abu, 0x3f3913b3u, 0x3f800000u,
-};
-
 enum Mode : int { kRef = 0, kSingle = 1, kBnb = 2, kBnbSingle = 3 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -96,6 +88,7 @@ struct Batch {
     Desc d[MAXB];
     uint32_t count;
     uint32_t total_tiles;
+    uint32_t seg_shift;  // tiles are split into 2^seg_shift contiguous segments, one per block residue
 };
 
 // Keep an fp32 product opaque to the backend: without this, hipcc folds
@@ -257,21 +250,45 @@ __device__ __forceinline__ uint32_t find_matrix(const Batch<MAXB>& bt, uint32_t 
     return k;
 }
 
-// Position of a wave in the launch: tile t of matrix k (packed byte `base`).
+// The 16 NF4 code points (fp32 bit patterns of kernel_optimized.py:234-239)
+// into LDS from immediates (no global load on the
+// kernel's critical path): thread 0 writes four 16-byte rows.
+__device__ __forceinline__ void write_lut(float* lut) {
+    if (threadIdx.x == 0) {
+        u32x4* l4 = reinterpret_cast<u32x4*>(lut);
+        l4[0] = u32x4{0xbf800000u, 0xbf3239b1u, 0xbf066b30u, 0xbeca32a0u};
+        l4[1] = u32x4{0xbe91a24du, 0xbe3d353fu, 0xbdba7871u, 0x00000000u};
+        l4[2] = u32x4{0x3da2faffu, 0x3e24cae3u, 0x3e7c04ddu, 0x3ead033au};
+        l4[3] = u32x4{0x3ee1a4b8u, 0x3f1007abu, 0x3f3913b3u, 0x3f800000u};
+    }
+}
+
+// Position of a wave in the launch: the i-th tile of its segment, which is
+// tile t of the launch = tile of matrix k starting at packed byte `base`.
 struct Cursor {
-    uint32_t t, k, base;
+    uint32_t i, t, k, base;
     bool valid;
 };
 
+// Segments: block b works in segment b % S (S = 2^seg_shift, the grid is a
+// multiple of S), so with S = 8 and the observed round-robin block placement
+// each XCD sweeps one contiguous region instead of all eight interleaving
+// through the same window (speed only: any placement is correct).
+struct SegMap {
+    uint32_t seg_base;  // first tile of this block's segment
+    uint32_t seg_tiles; // tiles per segment (last segment may be shorter)
+};
+
 template <int U, int MAXB>
-__device__ __forceinline__ Cursor cursor_at(const Batch<MAXB>& bt, uint32_t t, uint32_t k_hint) {
+__device__ __forceinline__ Cursor cursor_at(const Batch<MAXB>& bt, const SegMap& sm, uint32_t i, uint32_t k_hint) {
     constexpr uint32_t kTileBytes = 256u * U;
     Cursor c;
-    c.t = t;
-    c.valid = t < bt.total_tiles;
-    c.k = c.valid ? find_matrix(bt, t, k_hint) : k_hint;
+    c.i = i;
+    c.t = sm.seg_base + i;
+    c.valid = i < sm.seg_tiles && c.t < bt.total_tiles;
+    c.k = c.valid ? find_matrix(bt, c.t, k_hint) : k_hint;
     // past the end: an offset beyond every buffer range (loads return 0, stores drop)
-    c.base = c.valid ? (t - bt.d[c.k].tile_begin) * kTileBytes : 0xFFFFF000u;
+    c.base = c.valid ? (c.t - bt.d[c.k].tile_begin) * kTileBytes : 0xFFFFF000u;
     return c;
 }
 
@@ -290,16 +307,19 @@ __device__ __forceinline__ void make_rsrcs(const Batch<MAXB>& bt, uint32_t k, __
 // the loads it copies).
 template <int DT, int MODE, int U, int AUXS, int AUXL, int MAXB>
 __global__ __launch_bounds__(kWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
-    __shared__ float lut[16];
-    if (threadIdx.x < 16) lut[threadIdx.x] = __uint_as_float(kNf4Bits[threadIdx.x]);
-    __syncthreads();
-
+    __shared__ __attribute__((aligned(16))) float lut[16];
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWg + (threadIdx.x >> 6));
-    const uint32_t nwaves = gridDim.x * kWavesPerWg;
-    if (t0 >= bt.total_tiles) return;
+    const uint32_t sshift = bt.seg_shift;
+    SegMap sm;
+    sm.seg_tiles = (bt.total_tiles + (1u << sshift) - 1u) >> sshift;
+    sm.seg_base = (blockIdx.x & ((1u << sshift) - 1u)) * sm.seg_tiles;
+    const uint32_t i0 = __builtin_amdgcn_readfirstlane((blockIdx.x >> sshift) * kWavesPerWg + (threadIdx.x >> 6));
+    const uint32_t nwaves = (gridDim.x >> sshift) * kWavesPerWg;  // waves per segment
 
-    Cursor ca = cursor_at<U>(bt, t0, 0u);
+    // First tile's loads go out before anything else (a wave without work
+    // issues them past the buffer range: no traffic); the LUT write and the
+    // barrier then overlap their latency.
+    Cursor ca = cursor_at<U>(bt, sm, i0, 0u);
     __amdgpu_buffer_rsrc_t rpa, roa;
     make_rsrcs<DT>(bt, ca.k, rpa, roa);
     TileIn<U> A = tile_load<MODE, U, AUXL>(bt.d[ca.k], rpa, ca.base, lane);
@@ -312,15 +332,18 @@ __global__ __launch_bounds__(kWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
 #pragma unroll
         for (int j = 0; j < kStores; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, roa, 0xFFFFF000u + 16u * j, 0, AUXS);
     }
+    write_lut(lut);
+    __syncthreads();
+    if (!ca.valid) return;
     while (true) {
-        const Cursor cb = cursor_at<U>(bt, ca.t + nwaves, ca.k);
+        const Cursor cb = cursor_at<U>(bt, sm, ca.i + nwaves, ca.k);
         __amdgpu_buffer_rsrc_t rpb = rpa, rob = roa;
         if (MAXB > 1 && cb.k != ca.k) make_rsrcs<DT>(bt, cb.k, rpb, rob);
         const TileIn<U> B = tile_load<MODE, U, AUXL>(bt.d[cb.k], rpb, cb.base, lane);
         tile_finish<DT, MODE, U, AUXS>(bt.d[ca.k], roa, lut, A, ca.base, lane);
         if (!cb.valid) break;
 
-        const Cursor cn = cursor_at<U>(bt, cb.t + nwaves, cb.k);
+        const Cursor cn = cursor_at<U>(bt, sm, cb.i + nwaves, cb.k);
         __amdgpu_buffer_rsrc_t rpn = rpb, ron = rob;
         if (MAXB > 1 && cn.k != cb.k) make_rsrcs<DT>(bt, cn.k, rpn, ron);
         A = tile_load<MODE, U, AUXL>(bt.d[cn.k], rpn, cn.base, lane);
@@ -344,8 +367,8 @@ struct RowsArgs {
 
 template <int DT, int MODE>
 __global__ __launch_bounds__(kWg) void nf4_rows_kernel(const RowsArgs A) {
-    __shared__ float lut[16];
-    if (threadIdx.x < 16) lut[threadIdx.x] = __uint_as_float(kNf4Bits[threadIdx.x]);
+    __shared__ __attribute__((aligned(16))) float lut[16];
+    write_lut(lut);
     __syncthreads();
     const int64_t total = A.m * A.cols_b;
     for (int64_t i = (int64_t)blockIdx.x * kWg + threadIdx.x; i < total; i += (int64_t)gridDim.x * kWg) {
@@ -381,8 +404,8 @@ struct BnbBytesArgs {
 
 template <int DT>
 __global__ __launch_bounds__(kWg) void nf4_bnb_bytes_kernel(const BnbBytesArgs A) {
-    __shared__ float lut[16];
-    if (threadIdx.x < 16) lut[threadIdx.x] = __uint_as_float(kNf4Bits[threadIdx.x]);
+    __shared__ __attribute__((aligned(16))) float lut[16];
+    write_lut(lut);
     __syncthreads();
     const int64_t nbytes = (A.numel + 1) / 2;
     for (int64_t i = (int64_t)blockIdx.x * kWg + threadIdx.x; i < nbytes; i += (int64_t)gridDim.x * kWg) {
@@ -410,7 +433,7 @@ inline int ilog2(uint64_t v) {
     return s;
 }
 
-constexpr nf4_launch_cfg kDefaultCfg = {8, 0, 1, 0};
+constexpr nf4_launch_cfg kDefaultCfg = {4, 0, 1, 0};  // measured best at 4096^2 (tools/tune.py)
 
 int cu_count() {
     int dev = 0, cus = 0;
@@ -438,6 +461,10 @@ int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_laun
         const uint64_t cap = (uint64_t)cfg.blocks_per_cu * (uint64_t)cu_count();
         if (blocks > cap) blocks = cap;
     }
+    const uint32_t sshift = (uint32_t)((cfg.flags >> NF4DQ_CFG_SEG_SHIFT_BIT) & 0xF);
+    b.seg_shift = sshift;
+    const uint64_t S = uint64_t(1) << sshift;
+    blocks = (blocks + S - 1) / S * S;  // every segment gets the same number of blocks
     const dim3 grid((unsigned)blocks), block(kWg);
     const int auxs = cfg.nontemporal ? kAuxNt : 0;
     const int auxl = (cfg.flags & NF4DQ_CFG_NT_LOADS) ? kAuxNt : 0;
@@ -569,7 +596,8 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len, const uint8_t
                         const nf4_launch_cfg* cfg, void* hip_stream) {
     nf4_launch_cfg c = cfg ? *cfg : kDefaultCfg;
     if (c.tile_dwords != 4 && c.tile_dwords != 8) return NF4DQ_ERR_ARG;
-    if (c.flags & ~NF4DQ_CFG_NT_LOADS) return NF4DQ_ERR_ARG;
+    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_SEG_SHIFT_MASK)) return NF4DQ_ERR_ARG;
+    if (((c.flags >> NF4DQ_CFG_SEG_SHIFT_BIT) & 0xF) > 6) return NF4DQ_ERR_ARG;
     return ref_impl(packed, packed_len, absmax_q, nb, absmax2, n2, out, out_dtype, m, n, c,
                     reinterpret_cast<hipStream_t>(hip_stream));
 }

@@ -168,7 +168,8 @@ def test_batched_matches_single_calls(coracle, gpu):
 
 
 @pytest.mark.parametrize("cfg", [(4, 0, 0, 0), (8, 0, 0, 0), (4, 0, 1, 0), (8, 2, 1, 1), (4, 1, 0, 1), (8, 8, 0, 0),
-                                 (8, 1, 1, 0), (4, 3, 1, 1)])
+                                 (8, 1, 1, 0), (4, 3, 1, 1), (8, 0, 1, 0x300), (4, 2, 1, 0x100), (8, 1, 1, 0x600),
+                                 (8, 0, 1, 0x400)])
 def test_launch_configs_identical(coracle, gpu, cfg):
     from nf4_triton_dequantization_amd import _lib
 

@@ -57,7 +57,7 @@ def main():
     cfgs = [c for c in itertools.product([int(x) for x in args.tiles.split(",")],
                                          [int(x) for x in args.bpcu.split(",")],
                                          [int(x) for x in args.nt.split(",")],
-                                         [int(x) for x in args.flags.split(",")])]
+                                         [int(x, 0) for x in args.flags.split(",")])]
 
     def launch(i, cfg, sp):
         q, a1, a2, out = sets[i % P]
