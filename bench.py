@@ -45,7 +45,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from nf4_triton_dequantization_amd import _lib  # noqa: E402
-from nf4_triton_dequantization_amd.sharding import QuantStats, broadcast_quant_stats  # noqa: E402
+from nf4_triton_dequantization_amd.sharding import QuantStats, broadcast_quant_stats, max_over_ranks  # noqa: E402
 
 PEAK_HBM = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 ROUND = "r01"
@@ -237,9 +237,7 @@ def main():
         dist.barrier()
     t_ms = ev0.elapsed_time(ev1)
     if world > 1:
-        t = torch.tensor([t_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_ms = float(t.item())
+        t_ms = max_over_ranks(t_ms, dev)
 
     # ---- roofline: mean launch duration = HIP-event time of the timed region / K
     # (events on the launch stream; includes the inter-launch gaps, so it is an

@@ -89,3 +89,10 @@ def broadcast_quant_stats(stats: Optional[Sequence[QuantStats]], device: torch.d
         o1 += nb
         o2 += n2
     return out
+
+
+def max_over_ranks(x: float, device: torch.device, group=None) -> float:
+    """Max of a per-rank float over the group (bench timing: slowest rank decides)."""
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())

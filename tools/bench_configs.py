@@ -1,0 +1,133 @@
+"""Measure the BASELINE.json configs other than the bench.py headline, on one GPU.
+
+    python tools/bench_configs.py [--configs c3,c3b,c4,c5] [--reps 5] > profiles/r01/configs.jsonl
+
+c3   Llama-3-8B: 32 layers x {q,o 4096x4096; k,v 1024x4096; gate,up 14336x4096;
+     down 4096x14336} NF4->bf16, all 224 weights per pass through the batched
+     C ABI (nf4_dequant_ref_batched, <= NF4DQ_BATCH_MAX matrices per launch).
+c3b  the "4096/11008" shape set BASELINE names (Llama-2-7B: q,k,v,o 4096x4096;
+     gate,up 11008x4096; down 4096x11008), same method.
+c4   4096x4096 NF4 -> fp16 vs bf16 vs fp32 output, single launches over 16
+     rotating buffer sets, hipGraph replay.
+c5   one 8192x8192 NF4->bf16 matrix (the per-GPU unit of the 8-GPU config).
+
+Every line: elements/s and algorithmic GB/s (SURVEY §8d bytes) vs the 8 TB/s
+peak; timing = HIP events around the whole pass on the launch stream.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from nf4_triton_dequantization_amd import _lib  # noqa: E402
+
+PEAK = 8.0e12
+LLAMA3_8B = [(4096, 4096), (1024, 4096), (1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 14336)]
+LLAMA2_7B = [(4096, 4096)] * 4 + [(11008, 4096), (11008, 4096), (4096, 11008)]
+
+
+def alg_bytes(m, n, ob):
+    N = m * n
+    nb = N // 64
+    n2 = (nb + 255) // 256
+    g = ((n + 63) // 64 + 3) // 4
+    return N // 2 + N * ob + nb + 4 * min(n2, m * g)
+
+
+def make_weight(m, n, dev, gen, dt):
+    nb = m * n // 64
+    return (torch.randint(0, 256, (m * n // 2,), dtype=torch.uint8, device=dev, generator=gen),
+            torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen),
+            torch.rand((nb + 255) // 256, device=dev, generator=gen) * 0.01 + 1e-3,
+            torch.empty((m, n), dtype=dt, device=dev))
+
+
+def timed(fn, reps):
+    st = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = []
+    for _ in range(reps):
+        e0.record(st)
+        fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        best.append(e0.elapsed_time(e1) * 1e-3)
+    best.sort()
+    return best[len(best) // 2]
+
+
+def run_model(name, shapes, layers, reps, dev):
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0)
+    ws = [make_weight(m, n, dev, gen, torch.bfloat16) for _ in range(layers) for (m, n) in shapes]
+    descs = (_lib.MatrixDesc * len(ws))(*[
+        _lib.MatrixDesc(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                        o.data_ptr(), o.shape[0], o.shape[1]) for (q, a1, a2, o) in ws])
+    L = _lib.lib()
+
+    def fn():
+        rc = L.nf4_dequant_ref_batched(descs, len(ws), _lib.BF16, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, rc
+
+    t = timed(fn, reps)
+    elems = sum(o.numel() for *_, o in ws)
+    byt = sum(alg_bytes(o.shape[0], o.shape[1], 2) for *_, o in ws)
+    launches = -(-len(ws) // _lib.BATCH_MAX)
+    return {"config": name, "matrices": len(ws), "launches": launches, "elements": elems, "seconds": t,
+            "elements_per_s": elems / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK}
+
+
+def run_single(name, m, n, dt, code, reps, dev, sets=16, steps=64):
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    ws = [make_weight(m, n, dev, gen, dt) for _ in range(sets)]
+    L = _lib.lib()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        sp = torch.cuda.current_stream().cuda_stream
+        for i in range(steps):
+            q, a1, a2, o = ws[i % sets]
+            assert L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                                     o.data_ptr(), code, m, n, sp) == 0
+    t = timed(graph.replay, reps) / steps
+    ob = torch.empty((), dtype=dt).element_size()
+    byt = alg_bytes(m, n, ob)
+    return {"config": name, "m": m, "n": n, "out_dtype": str(dt).replace("torch.", ""), "us_per_launch": t * 1e6,
+            "elements_per_s": m * n / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3,c3b,c4,c5")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--layers", type=int, default=32)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    todo = args.configs.split(",")
+    if "c3" in todo:
+        print(json.dumps(run_model("c3 Llama-3-8B linears x32 NF4->bf16 batched", LLAMA3_8B, args.layers, args.reps,
+                                   dev)), flush=True)
+        torch.cuda.empty_cache()
+    if "c3b" in todo:
+        print(json.dumps(run_model("c3b Llama-2-7B (4096/11008) linears x32 NF4->bf16 batched", LLAMA2_7B,
+                                   args.layers, args.reps, dev)), flush=True)
+        torch.cuda.empty_cache()
+    if "c4" in todo:
+        for dt, code in ((torch.float16, _lib.F16), (torch.bfloat16, _lib.BF16), (torch.float32, _lib.F32)):
+            print(json.dumps(run_single("c4 4096x4096 dtype sweep", 4096, 4096, dt, code, args.reps, dev)), flush=True)
+    if "c5" in todo:
+        print(json.dumps(run_single("c5 8192x8192 per-GPU unit", 8192, 8192, torch.bfloat16, _lib.BF16, args.reps, dev,
+                                    sets=8, steps=32)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
