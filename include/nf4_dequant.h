@@ -94,15 +94,19 @@ int nf4_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t n
                            void* out, int32_t out_dtype, int64_t numel,
                            int32_t blocksize, void* hip_stream);
 
-/* Launch tuning (bench/tuning only; the entry points above use defaults).
- * tile_dwords: 4 or 8 packed dwords per lane per tile; blocks_per_cu: grid cap
- * per CU (0 = one workgroup per 4 tiles, no cap); nontemporal: 0/1 streaming
- * (nt) output stores; flags: NF4DQ_CFG_* bits. */
+/* Launch tuning (bench/tuning only; the entry points above use the default
+ * {4, 0, 1, 0}).  tile_dwords: 4 or 8 packed dwords per lane per tile;
+ * blocks_per_cu: grid cap per CU (0 = one wave per tile, no cap); nontemporal:
+ * 0/1 streaming (nt) output stores; flags: NF4DQ_CFG_* bits.  Non-default
+ * tile/nt-load/workgroup settings exist for fp16/bf16 reference semantics. */
 #define NF4DQ_CFG_NT_LOADS 1   /* nt cache policy on the packed-weight loads */
 /* bits 8..11: log2 of the number of contiguous tile segments (0..6); block b
  * works in segment b % 2^k (k = 3: one segment per XCD under round-robin placement) */
 #define NF4DQ_CFG_SEG_SHIFT_BIT 8
 #define NF4DQ_CFG_SEG_SHIFT_MASK 0xF00
+/* bits 4..7: log2 of waves per workgroup (0 = default 4; 1, 2, 3, 4 = 2, 4, 8, 16) */
+#define NF4DQ_CFG_WG_SHIFT_BIT 4
+#define NF4DQ_CFG_WG_SHIFT_MASK 0xF0
 typedef struct nf4_launch_cfg {
     int32_t tile_dwords;
     int32_t blocks_per_cu;

@@ -145,8 +145,7 @@ __device__ __forceinline__ float block_scale(const Desc& D, uint32_t g) {
     }
 }
 
-constexpr int kWg = 256;  // 4 waves
-constexpr int kWavesPerWg = kWg / 64;
+constexpr int kWg = 256;  // 4 waves (rows / bytes kernels; the flat kernel takes WPG)
 
 // Cache-policy bits of the buffer instructions (aux operand): 2 = nt (streaming).
 constexpr int kAuxNt = 2;
@@ -154,6 +153,13 @@ constexpr int kRsrcFlags = 0x00020000;  // raw buffer, dword format (gfx950)
 
 template <int DT>
 constexpr uint32_t out_bytes_per_packed_byte() { return DT == NF4DQ_F32 ? 8u : 4u; }
+// Packed bytes a lane loads per step j: 4 (-> 8 outputs = 16 B of fp16/bf16) or,
+// for fp32 output, 2 (-> 4 outputs = 16 B).  Either way every lane stores 16 B
+// per step and a wave store instruction covers 1 KiB contiguous.
+template <int DT>
+constexpr uint32_t lane_bytes() { return DT == NF4DQ_F32 ? 2u : 4u; }
+template <int DT, int U>
+constexpr uint32_t tile_bytes() { return 64u * lane_bytes<DT>() * U; }
 
 // Raw inputs of one wave-tile, loaded ahead of use (software pipeline stage 1).
 template <int U>
@@ -166,15 +172,21 @@ struct TileIn {
 
 // Issue the loads of tile `base` (packed bytes) of matrix D.  Buffer loads
 // outside the matrix return 0, so partial tiles need no predicates.
-template <int MODE, int U, int AUXL>
+template <int DT, int MODE, int U, int AUXL>
 __device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rsrc_t rp, uint32_t base,
                                                uint32_t lane) {
+    constexpr uint32_t LB = lane_bytes<DT>();
     TileIn<U> in;
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-        in.w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, base + 256u * j + 4u * lane, 0, AUXL);
+        const uint32_t off = base + 64u * LB * j + LB * lane;
+        if constexpr (LB == 4) {
+            in.w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, AUXL);
+        } else {
+            in.w[j] = __builtin_amdgcn_raw_buffer_load_b16(rp, off, 0, AUXL);
+        }
     }
-    constexpr uint32_t kTileBytes = 256u * U;
+    constexpr uint32_t kTileBytes = tile_bytes<DT, U>();
     const uint32_t bsh = D.blk_shift;
     const uint32_t bpt = kTileBytes >> bsh;  // 0 when one block spans the tile
     uint32_t g = (base >> bsh) + (bpt ? (lane & (bpt - 1u)) : 0u);
@@ -215,26 +227,25 @@ __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_
     }
     const uint32_t bsh = D.blk_shift;
     constexpr uint32_t kOB = out_bytes_per_packed_byte<DT>();
+    constexpr uint32_t LB = lane_bytes<DT>();
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-        const uint32_t rel = 256u * j + 4u * lane;
+        const uint32_t rel = 64u * LB * j + LB * lane;
         const float sj = __shfl(s, (int)(rel >> bsh), 64);
         const uint32_t w = in.w[j];
         const uint32_t hi4 = (w >> 2) & 0x3C3C3C3Cu;
         const uint32_t lo4 = (w << 2) & 0x3C3C3C3Cu;
         const char* t = reinterpret_cast<const char*>(lut);
-        float v[8];
+        float v[2 * LB];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < (int)LB; ++k) {
             v[2 * k] = *reinterpret_cast<const float*>(t + ((hi4 >> (8 * k)) & 0xFFu)) * sj;
             v[2 * k + 1] = *reinterpret_cast<const float*>(t + ((lo4 >> (8 * k)) & 0xFFu)) * sj;
         }
         const uint32_t ob = (base + rel) * kOB;
         if constexpr (DT == NF4DQ_F32) {
-            u32x4 o0 = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-            u32x4 o1 = {__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
-            __builtin_amdgcn_raw_buffer_store_b128(o0, ro, ob, 0, AUXS);
-            __builtin_amdgcn_raw_buffer_store_b128(o1, ro, ob + 16u, 0, AUXS);
+            u32x4 o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(o, ro, ob, 0, AUXS);
         } else {
             u32x4 o = {pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7])};
             __builtin_amdgcn_raw_buffer_store_b128(o, ro, ob, 0, AUXS);
@@ -279,9 +290,9 @@ struct SegMap {
     uint32_t seg_tiles; // tiles per segment (last segment may be shorter)
 };
 
-template <int U, int MAXB>
+template <int DT, int U, int MAXB>
 __device__ __forceinline__ Cursor cursor_at(const Batch<MAXB>& bt, const SegMap& sm, uint32_t i, uint32_t k_hint) {
-    constexpr uint32_t kTileBytes = 256u * U;
+    constexpr uint32_t kTileBytes = tile_bytes<DT, U>();
     Cursor c;
     c.i = i;
     c.t = sm.seg_base + i;
@@ -305,29 +316,29 @@ __device__ __forceinline__ void make_rsrcs(const Batch<MAXB>& bt, uint32_t k, __
 // register sets (A, B) so that tile i+1's loads are in flight while tile i is
 // decoded and stored, with no register copies (a copy would force a wait on
 // the loads it copies).
-template <int DT, int MODE, int U, int AUXS, int AUXL, int MAXB>
-__global__ __launch_bounds__(kWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
+template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB>
+__global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt) {
     __shared__ __attribute__((aligned(16))) float lut[16];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t sshift = bt.seg_shift;
     SegMap sm;
     sm.seg_tiles = (bt.total_tiles + (1u << sshift) - 1u) >> sshift;
     sm.seg_base = (blockIdx.x & ((1u << sshift) - 1u)) * sm.seg_tiles;
-    const uint32_t i0 = __builtin_amdgcn_readfirstlane((blockIdx.x >> sshift) * kWavesPerWg + (threadIdx.x >> 6));
-    const uint32_t nwaves = (gridDim.x >> sshift) * kWavesPerWg;  // waves per segment
+    const uint32_t i0 = __builtin_amdgcn_readfirstlane((blockIdx.x >> sshift) * WPG + (threadIdx.x >> 6));
+    const uint32_t nwaves = (gridDim.x >> sshift) * WPG;  // waves per segment
 
     // First tile's loads go out before anything else (a wave without work
     // issues them past the buffer range: no traffic); the LUT write and the
     // barrier then overlap their latency.
-    Cursor ca = cursor_at<U>(bt, sm, i0, 0u);
+    Cursor ca = cursor_at<DT, U>(bt, sm, i0, 0u);
     __amdgpu_buffer_rsrc_t rpa, roa;
     make_rsrcs<DT>(bt, ca.k, rpa, roa);
-    TileIn<U> A = tile_load<MODE, U, AUXL>(bt.d[ca.k], rpa, ca.base, lane);
+    TileIn<U> A = tile_load<DT, MODE, U, AUXL>(bt.d[ca.k], rpa, ca.base, lane);
     // Out-of-range (dropped) stores with the loop body's count: loop entry then
     // looks like the back edge to hipcc's waitcnt pass ([loads][stores]), so the
     // in-loop waits count past the previous tile's stores instead of draining them.
     {
-        constexpr int kStores = DT == NF4DQ_F32 ? 2 * U : U;
+        constexpr int kStores = U;
         const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int j = 0; j < kStores; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, roa, 0xFFFFF000u + 16u * j, 0, AUXS);
@@ -336,17 +347,17 @@ __global__ __launch_bounds__(kWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
     __syncthreads();
     if (!ca.valid) return;
     while (true) {
-        const Cursor cb = cursor_at<U>(bt, sm, ca.i + nwaves, ca.k);
+        const Cursor cb = cursor_at<DT, U>(bt, sm, ca.i + nwaves, ca.k);
         __amdgpu_buffer_rsrc_t rpb = rpa, rob = roa;
         if (MAXB > 1 && cb.k != ca.k) make_rsrcs<DT>(bt, cb.k, rpb, rob);
-        const TileIn<U> B = tile_load<MODE, U, AUXL>(bt.d[cb.k], rpb, cb.base, lane);
+        const TileIn<U> B = tile_load<DT, MODE, U, AUXL>(bt.d[cb.k], rpb, cb.base, lane);
         tile_finish<DT, MODE, U, AUXS>(bt.d[ca.k], roa, lut, A, ca.base, lane);
         if (!cb.valid) break;
 
-        const Cursor cn = cursor_at<U>(bt, sm, cb.i + nwaves, cb.k);
+        const Cursor cn = cursor_at<DT, U>(bt, sm, cb.i + nwaves, cb.k);
         __amdgpu_buffer_rsrc_t rpn = rpb, ron = rob;
         if (MAXB > 1 && cn.k != cb.k) make_rsrcs<DT>(bt, cn.k, rpn, ron);
-        A = tile_load<MODE, U, AUXL>(bt.d[cn.k], rpn, cn.base, lane);
+        A = tile_load<DT, MODE, U, AUXL>(bt.d[cn.k], rpn, cn.base, lane);
         tile_finish<DT, MODE, U, AUXS>(bt.d[cb.k], rob, lut, B, cb.base, lane);
         if (!cn.valid) break;
         ca = cn;
@@ -442,21 +453,58 @@ int cu_count() {
     return cus;
 }
 
+// Launch one flat batch.  Tile offsets are (re)computed here for the tile size
+// of (dtype, U); callers only fill the per-matrix descriptors.  The default
+// configuration instantiates for every dtype and scale mode; the tuning knobs
+// (U = 8, nt loads, workgroup size) exist for reference semantics in fp16/bf16.
+template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB>
+void launch_one(const Batch<MAXB>& b, uint64_t blocks, hipStream_t st) {
+    hipLaunchKernelGGL((nf4_flat_kernel<DT, MODE, U, AUXS, AUXL, WPG, MAXB>), dim3((unsigned)blocks),
+                       dim3(64 * WPG), 0, st, b);
+}
+
+template <int DT, int MAXB>
+int launch_tuned(const Batch<MAXB>& b, uint64_t blocks, uint32_t U, bool ntl, int wpg, hipStream_t st) {
+#define NF4_T(U_, AL_, W_) launch_one<DT, kRef, U_, kAuxNt, AL_, W_, MAXB>(b, blocks, st)
+#define NF4_W(U_, AL_)                        \
+    do {                                      \
+        if (wpg == 8) NF4_T(U_, AL_, 8);      \
+        else if (wpg == 16) NF4_T(U_, AL_, 16); \
+        else if (wpg == 2) NF4_T(U_, AL_, 2); \
+        else NF4_T(U_, AL_, 4);               \
+    } while (0)
+    if (U == 8) {
+        if (ntl) NF4_W(8, kAuxNt);
+        else NF4_W(8, 0);
+    } else {
+        if (ntl) NF4_W(4, kAuxNt);
+        else NF4_W(4, 0);
+    }
+#undef NF4_W
+#undef NF4_T
+    return NF4DQ_OK;
+}
+
 template <int MAXB>
 int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_launch_cfg& cfg, hipStream_t st) {
-    if (bt.total_tiles == 0) return NF4DQ_OK;
+    if (bt.count == 0) return NF4DQ_OK;
     const uint32_t U = cfg.tile_dwords == 8 ? 8u : 4u;
-    // total_tiles was counted with 1 KiB tiles; a 2 KiB tile covers two of them.
+    const bool ntl = (cfg.flags & NF4DQ_CFG_NT_LOADS) != 0;
+    const int wpg_log = (int)((cfg.flags >> NF4DQ_CFG_WG_SHIFT_BIT) & 0xF);
+    const int wpg = wpg_log ? (1 << wpg_log) : 4;
+    const bool tuned = U != 4 || ntl || wpg != 4 || !cfg.nontemporal;
+    if (tuned && (mode != kRef || dtype == NF4DQ_F32)) return NF4DQ_ERR_ARG;
+    const uint32_t lb = dtype == NF4DQ_F32 ? 2u : 4u;
+    const uint32_t tb = 64u * lb * U;
     Batch<MAXB> b = bt;
-    if (U == 8) {
-        uint32_t acc = 0;
-        for (uint32_t i = 0; i < b.count; ++i) {
-            b.d[i].tile_begin = acc;
-            acc += (b.d[i].nbytes + 2047u) / 2048u;
-        }
-        b.total_tiles = acc;
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < b.count; ++i) {
+        b.d[i].tile_begin = acc;
+        acc += (b.d[i].nbytes + tb - 1u) / tb;
     }
-    uint64_t blocks = (b.total_tiles + kWavesPerWg - 1) / kWavesPerWg;
+    b.total_tiles = acc;
+    if (acc == 0) return NF4DQ_OK;
+    uint64_t blocks = (acc + wpg - 1) / wpg;
     if (cfg.blocks_per_cu > 0) {
         const uint64_t cap = (uint64_t)cfg.blocks_per_cu * (uint64_t)cu_count();
         if (blocks > cap) blocks = cap;
@@ -465,41 +513,29 @@ int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_laun
     b.seg_shift = sshift;
     const uint64_t S = uint64_t(1) << sshift;
     blocks = (blocks + S - 1) / S * S;  // every segment gets the same number of blocks
-    const dim3 grid((unsigned)blocks), block(kWg);
-    const int auxs = cfg.nontemporal ? kAuxNt : 0;
-    const int auxl = (cfg.flags & NF4DQ_CFG_NT_LOADS) ? kAuxNt : 0;
 
-#define NF4_LAUNCH(DT_, MODE_, U_, AS_, AL_) \
-    hipLaunchKernelGGL((nf4_flat_kernel<DT_, MODE_, U_, AS_, AL_, MAXB>), grid, block, 0, st, b)
-#define NF4_DISPATCH_AUX(DT_, MODE_, U_)                       \
-    do {                                                       \
-        if (auxs && auxl) NF4_LAUNCH(DT_, MODE_, U_, kAuxNt, kAuxNt); \
-        else if (auxs) NF4_LAUNCH(DT_, MODE_, U_, kAuxNt, 0);  \
-        else if (auxl) NF4_LAUNCH(DT_, MODE_, U_, 0, kAuxNt);  \
-        else NF4_LAUNCH(DT_, MODE_, U_, 0, 0);                 \
+    if (tuned && !cfg.nontemporal) {
+        if (dtype == NF4DQ_BF16) launch_one<NF4DQ_BF16, kRef, 4, 0, 0, 4, MAXB>(b, blocks, st);
+        else launch_one<NF4DQ_F16, kRef, 4, 0, 0, 4, MAXB>(b, blocks, st);
+        if (U != 4 || ntl || wpg != 4) return NF4DQ_ERR_ARG;  // default-policy stores: base shape only
+    } else if (tuned) {
+        if (dtype == NF4DQ_BF16) launch_tuned<NF4DQ_BF16>(b, blocks, U, ntl, wpg, st);
+        else launch_tuned<NF4DQ_F16>(b, blocks, U, ntl, wpg, st);
+    } else {
+#define NF4_D(DT_)                                                                                    \
+    do {                                                                                              \
+        switch (mode) {                                                                               \
+            case kRef: launch_one<DT_, kRef, 4, kAuxNt, 0, 4, MAXB>(b, blocks, st); break;            \
+            case kSingle: launch_one<DT_, kSingle, 4, kAuxNt, 0, 4, MAXB>(b, blocks, st); break;      \
+            case kBnb: launch_one<DT_, kBnb, 4, kAuxNt, 0, 4, MAXB>(b, blocks, st); break;            \
+            default: launch_one<DT_, kBnbSingle, 4, kAuxNt, 0, 4, MAXB>(b, blocks, st); break;        \
+        }                                                                                             \
     } while (0)
-#define NF4_DISPATCH_U(DT_, MODE_)                                 \
-    do {                                                           \
-        if (U == 8) NF4_DISPATCH_AUX(DT_, MODE_, 8);               \
-        else NF4_DISPATCH_AUX(DT_, MODE_, 4);                      \
-    } while (0)
-#define NF4_DISPATCH_MODE(DT_)                                    \
-    do {                                                          \
-        switch (mode) {                                           \
-            case kRef: NF4_DISPATCH_U(DT_, kRef); break;          \
-            case kSingle: NF4_DISPATCH_U(DT_, kSingle); break;    \
-            case kBnb: NF4_DISPATCH_U(DT_, kBnb); break;          \
-            default: NF4_DISPATCH_U(DT_, kBnbSingle); break;      \
-        }                                                         \
-    } while (0)
-
-    if (dtype == NF4DQ_BF16) NF4_DISPATCH_MODE(NF4DQ_BF16);
-    else if (dtype == NF4DQ_F16) NF4_DISPATCH_MODE(NF4DQ_F16);
-    else NF4_DISPATCH_MODE(NF4DQ_F32);
-#undef NF4_DISPATCH_MODE
-#undef NF4_DISPATCH_U
-#undef NF4_DISPATCH_AUX
-#undef NF4_LAUNCH
+        if (dtype == NF4DQ_BF16) NF4_D(NF4DQ_BF16);
+        else if (dtype == NF4DQ_F16) NF4_D(NF4DQ_F16);
+        else NF4_D(NF4DQ_F32);
+#undef NF4_D
+    }
     return hip_rc(hipGetLastError());
 }
 
@@ -596,8 +632,11 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len, const uint8_t
                         const nf4_launch_cfg* cfg, void* hip_stream) {
     nf4_launch_cfg c = cfg ? *cfg : kDefaultCfg;
     if (c.tile_dwords != 4 && c.tile_dwords != 8) return NF4DQ_ERR_ARG;
-    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_SEG_SHIFT_MASK)) return NF4DQ_ERR_ARG;
+    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_SEG_SHIFT_MASK | NF4DQ_CFG_WG_SHIFT_MASK)) return NF4DQ_ERR_ARG;
     if (((c.flags >> NF4DQ_CFG_SEG_SHIFT_BIT) & 0xF) > 6) return NF4DQ_ERR_ARG;
+    if (((c.flags >> NF4DQ_CFG_WG_SHIFT_BIT) & 0xF) > 4) return NF4DQ_ERR_ARG;
+    if (!c.nontemporal && (c.tile_dwords != 4 || (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_WG_SHIFT_MASK))))
+        return NF4DQ_ERR_ARG;
     return ref_impl(packed, packed_len, absmax_q, nb, absmax2, n2, out, out_dtype, m, n, c,
                     reinterpret_cast<hipStream_t>(hip_stream));
 }

@@ -167,9 +167,10 @@ def test_batched_matches_single_calls(coracle, gpu):
         assert_bits_equal(out_bits(o), w, "f16", f"batched #{i}")
 
 
-@pytest.mark.parametrize("cfg", [(4, 0, 0, 0), (8, 0, 0, 0), (4, 0, 1, 0), (8, 2, 1, 1), (4, 1, 0, 1), (8, 8, 0, 0),
+@pytest.mark.parametrize("cfg", [(4, 0, 0, 0), (4, 0, 1, 0), (8, 0, 1, 0), (8, 2, 1, 1), (4, 1, 1, 1), (8, 8, 1, 0),
                                  (8, 1, 1, 0), (4, 3, 1, 1), (8, 0, 1, 0x300), (4, 2, 1, 0x100), (8, 1, 1, 0x600),
-                                 (8, 0, 1, 0x400)])
+                                 (8, 0, 1, 0x400), (4, 0, 1, 0x30), (8, 0, 1, 0x40), (4, 0, 1, 0x10),
+                                 (4, 0, 0, 0x300), (8, 3, 1, 0x331)])
 def test_launch_configs_identical(coracle, gpu, cfg):
     from nf4_triton_dequantization_amd import _lib
 
