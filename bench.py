@@ -117,15 +117,22 @@ def main():
     ap.add_argument("--flags", type=int, default=0, help="NF4DQ_CFG_* bits (1 = nt loads)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for real runs; gloo to rehearse")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # rehearsal on a box with fewer GPUs than ranks (gloo only): ranks share devices
+    ndev = torch.cuda.device_count()
+    local_dev = local if args.dist_backend == "nccl" else local % max(1, ndev)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     m, n, P = args.m, args.n, args.sets
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
@@ -281,7 +288,7 @@ def main():
             "buffer_sets": P, "launch": "hipGraph" if graph is not None else "eager",
             "streams": args.streams, "tile_dwords": args.tile_dwords, "blocks_per_cu": args.blocks_per_cu,
             "nontemporal": args.nontemporal, "flags": args.flags, "parallelism": f"shard{world} (independent matrices)",
-            "quant_state_broadcast_ms": round(bcast_ms, 3),
+            "quant_state_broadcast_ms": round(bcast_ms, 3), "dist_backend": args.dist_backend if world > 1 else None,
         },
         "roofline": {
             "bound": "hbm",
