@@ -97,7 +97,7 @@ int nf4_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t n
 /* Launch tuning (bench/tuning only; the entry points above use the default
  * {4, 0, 1, 0}).  tile_dwords: 4 or 8 packed dwords per lane per tile;
  * blocks_per_cu: grid cap per CU (0 = one wave per tile, no cap); nontemporal:
- * 0/1 streaming (nt) output stores; flags: NF4DQ_CFG_* bits.  Non-default
+ * 0 = default-policy output stores, 1 = streaming (sc1+nt) stores; flags: NF4DQ_CFG_* bits.  Non-default
  * tile/nt-load/workgroup settings exist for fp16/bf16 reference semantics. */
 #define NF4DQ_CFG_NT_LOADS 1   /* nt cache policy on the packed-weight loads */
 /* bits 8..11: log2 of the number of contiguous tile segments (0..6); block b
@@ -107,6 +107,10 @@ int nf4_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t n
 /* bits 4..7: log2 of waves per workgroup (0 = default 4; 1, 2, 3, 4 = 2, 4, 8, 16) */
 #define NF4DQ_CFG_WG_SHIFT_BIT 4
 #define NF4DQ_CFG_WG_SHIFT_MASK 0xF0
+/* bits 12..15: output-store cache policy experiment (0 = default sc1+nt; 1 nt,
+ * 2 sc0+nt, 3 sc0+sc1+nt, 4 sc1, 5 sc0+sc1); base tile shape only */
+#define NF4DQ_CFG_STORE_POLICY_BIT 12
+#define NF4DQ_CFG_STORE_POLICY_MASK 0xF000
 typedef struct nf4_launch_cfg {
     int32_t tile_dwords;
     int32_t blocks_per_cu;
