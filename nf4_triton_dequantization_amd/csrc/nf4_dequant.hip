@@ -176,11 +176,21 @@ struct TileIn {
 
 // Issue the loads of tile `base` (packed bytes) of matrix D.  Buffer loads
 // outside the matrix return 0, so partial tiles need no predicates.
-template <int DT, int MODE, int U, int AUXL>
+template <int DT, int MODE, int U, int AUXL, int X4 = 0>
 __device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rsrc_t rp, uint32_t base,
                                                uint32_t lane) {
     constexpr uint32_t LB = lane_bytes<DT>();
     TileIn<U> in;
+    if constexpr (X4) {
+        // one 16-byte load per lane (1 KiB per wave instruction); tile_finish
+        // redistributes through LDS into the store-friendly dword order
+        static_assert(U == 4 && LB == 4, "x4 loads: base tile shape only");
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, base + 16u * lane, 0, AUXL);
+        in.w[0] = v.x;
+        in.w[1] = v.y;
+        in.w[2] = v.z;
+        in.w[3] = v.w;
+    } else
 #pragma unroll
     for (int j = 0; j < U; ++j) {
         const uint32_t off = base + 64u * LB * j + LB * lane;
@@ -218,9 +228,19 @@ __device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rs
 // round, and U 16-byte stores (fp32: 2U) -- each wave store instruction writes
 // 1 KiB contiguous; stores past the end of the matrix are dropped by the buffer
 // range check.
-template <int DT, int MODE, int U, int AUXS>
+template <int DT, int MODE, int U, int AUXS, int X4 = 0>
 __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_t ro, const float* lut,
-                                            const TileIn<U>& in, uint32_t base, uint32_t lane) {
+                                            const TileIn<U>& in_, uint32_t base, uint32_t lane,
+                                            uint32_t* stage = nullptr) {
+    TileIn<U> in = in_;
+    if constexpr (X4) {
+        // lane l holds packed bytes [16l, 16l+16); the store layout wants dword
+        // j of lane l = bytes [256j + 4l, +4).  One ds_write_b128 + four
+        // ds_read_b32 on this wave's private 1 KiB slice (in-order per wave).
+        reinterpret_cast<u32x4*>(stage)[lane] = u32x4{in.w[0], in.w[1], in.w[2], in.w[3]};
+#pragma unroll
+        for (int j = 0; j < U; ++j) in.w[j] = stage[64 * j + lane];
+    }
     float s;
     if constexpr (MODE == kRef) {
         s = ((float)in.a1 / 127.0f) * in.a2;  // IEEE division (:45, :270), then fp32 multiply
@@ -320,9 +340,11 @@ __device__ __forceinline__ void make_rsrcs(const Batch<MAXB>& bt, uint32_t k, __
 // register sets (A, B) so that tile i+1's loads are in flight while tile i is
 // decoded and stored, with no register copies (a copy would force a wait on
 // the loads it copies).
-template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB>
+template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB, int X4 = 0>
 __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt) {
     __shared__ __attribute__((aligned(16))) float lut[16];
+    __shared__ __attribute__((aligned(16))) uint32_t stage_all[X4 ? WPG * 256 : 1];
+    uint32_t* stage = stage_all + (X4 ? (threadIdx.x >> 6) * 256 : 0);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t sshift = bt.seg_shift;
     SegMap sm;
@@ -337,7 +359,7 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
     Cursor ca = cursor_at<DT, U>(bt, sm, i0, 0u);
     __amdgpu_buffer_rsrc_t rpa, roa;
     make_rsrcs<DT>(bt, ca.k, rpa, roa);
-    TileIn<U> A = tile_load<DT, MODE, U, AUXL>(bt.d[ca.k], rpa, ca.base, lane);
+    TileIn<U> A = tile_load<DT, MODE, U, AUXL, X4>(bt.d[ca.k], rpa, ca.base, lane);
     // Out-of-range (dropped) stores with the loop body's count: loop entry then
     // looks like the back edge to hipcc's waitcnt pass ([loads][stores]), so the
     // in-loop waits count past the previous tile's stores instead of draining them.
@@ -354,15 +376,15 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
         const Cursor cb = cursor_at<DT, U>(bt, sm, ca.i + nwaves, ca.k);
         __amdgpu_buffer_rsrc_t rpb = rpa, rob = roa;
         if (MAXB > 1 && cb.k != ca.k) make_rsrcs<DT>(bt, cb.k, rpb, rob);
-        const TileIn<U> B = tile_load<DT, MODE, U, AUXL>(bt.d[cb.k], rpb, cb.base, lane);
-        tile_finish<DT, MODE, U, AUXS>(bt.d[ca.k], roa, lut, A, ca.base, lane);
+        const TileIn<U> B = tile_load<DT, MODE, U, AUXL, X4>(bt.d[cb.k], rpb, cb.base, lane);
+        tile_finish<DT, MODE, U, AUXS, X4>(bt.d[ca.k], roa, lut, A, ca.base, lane, stage);
         if (!cb.valid) break;
 
         const Cursor cn = cursor_at<DT, U>(bt, sm, cb.i + nwaves, cb.k);
         __amdgpu_buffer_rsrc_t rpn = rpb, ron = rob;
         if (MAXB > 1 && cn.k != cb.k) make_rsrcs<DT>(bt, cn.k, rpn, ron);
-        A = tile_load<DT, MODE, U, AUXL>(bt.d[cn.k], rpn, cn.base, lane);
-        tile_finish<DT, MODE, U, AUXS>(bt.d[cb.k], rob, lut, B, cb.base, lane);
+        A = tile_load<DT, MODE, U, AUXL, X4>(bt.d[cn.k], rpn, cn.base, lane);
+        tile_finish<DT, MODE, U, AUXS, X4>(bt.d[cb.k], rob, lut, B, cb.base, lane, stage);
         if (!cn.valid) break;
         ca = cn;
         rpa = rpn;
@@ -461,9 +483,9 @@ int cu_count() {
 // of (dtype, U); callers only fill the per-matrix descriptors.  The default
 // configuration instantiates for every dtype and scale mode; the tuning knobs
 // (U = 8, nt loads, workgroup size) exist for reference semantics in fp16/bf16.
-template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB>
+template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB, int X4 = 0>
 void launch_one(const Batch<MAXB>& b, uint64_t blocks, hipStream_t st) {
-    hipLaunchKernelGGL((nf4_flat_kernel<DT, MODE, U, AUXS, AUXL, WPG, MAXB>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((nf4_flat_kernel<DT, MODE, U, AUXS, AUXL, WPG, MAXB, X4>), dim3((unsigned)blocks),
                        dim3(64 * WPG), 0, st, b);
 }
 
@@ -519,6 +541,17 @@ int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_laun
     blocks = (blocks + S - 1) / S * S;  // every segment gets the same number of blocks
 
     const uint32_t pol = (uint32_t)((cfg.flags >> NF4DQ_CFG_STORE_POLICY_BIT) & 0xF);
+    if (cfg.flags & NF4DQ_CFG_X4_LOADS) {  // 16 B/lane loads + LDS redistribution: base shape only
+        if (U != 4 || wpg != 4 || !cfg.nontemporal || pol) return NF4DQ_ERR_ARG;
+        if (dtype == NF4DQ_BF16) {
+            if (ntl) launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, kAuxNt, 4, MAXB, 1>(b, blocks, st);
+            else launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, 0, 4, MAXB, 1>(b, blocks, st);
+        } else {
+            if (ntl) launch_one<NF4DQ_F16, kRef, 4, kAuxStore, kAuxNt, 4, MAXB, 1>(b, blocks, st);
+            else launch_one<NF4DQ_F16, kRef, 4, kAuxStore, 0, 4, MAXB, 1>(b, blocks, st);
+        }
+        return hip_rc(hipGetLastError());
+    }
     if (pol) {  // store cache-policy experiments: base shape, reference semantics, fp16/bf16
         if (U != 4 || ntl || wpg != 4 || !cfg.nontemporal) return NF4DQ_ERR_ARG;
 #define NF4_P(A_)                                                                         \
@@ -654,7 +687,7 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len, const uint8_t
                         const nf4_launch_cfg* cfg, void* hip_stream) {
     nf4_launch_cfg c = cfg ? *cfg : kDefaultCfg;
     if (c.tile_dwords != 4 && c.tile_dwords != 8) return NF4DQ_ERR_ARG;
-    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_SEG_SHIFT_MASK | NF4DQ_CFG_WG_SHIFT_MASK |
+    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_SEG_SHIFT_MASK | NF4DQ_CFG_WG_SHIFT_MASK |
                     NF4DQ_CFG_STORE_POLICY_MASK))
         return NF4DQ_ERR_ARG;
     if (((c.flags >> NF4DQ_CFG_SEG_SHIFT_BIT) & 0xF) > 6) return NF4DQ_ERR_ARG;

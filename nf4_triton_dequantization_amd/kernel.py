@@ -170,10 +170,10 @@ def dequantize_nf4_many(modules: Iterable) -> List[torch.Tensor]:
         with torch.cuda.device(device):
             rc = L.nf4_dequant_ref_batched(arr, len(descs), code, _stream_ptr(device))
         _lib.check(rc, "nf4 batched dequantize")
-    if keep:
-        # the launches read q/a1/a2 asynchronously: tie their lifetime to the stream
-        for t in keep:
-            t.record_stream(torch.cuda.current_stream(t.device))
+    # Temporaries in `keep` (value casts) were allocated on the stream the
+    # launches use, so the caching allocator's stream-ordered reuse already
+    # protects them; no record_stream needed (and it would break graph capture).
+    del keep
     return outs  # type: ignore[return-value]
 
 

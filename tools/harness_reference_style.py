@@ -1,0 +1,111 @@
+"""The reference harness's timed loop, replayed on MI355X with this path.
+
+Restates the measurement of the reference's benchmark.py (:86-138): for each of
+its three MLP configs (hd, m, dtype) = (2048, 8192, fp16), (1024, 4096, bf16),
+(4096, 14336, bf16), three Linear4bit weights (gate, up: m x hd; down: hd x m)
+are dequantized per iteration on three fresh streams (:68-84, ``.t()`` of each
+result), ``iterations`` times between two events; the total seconds is the
+number the reference compares against unsloth.  unsloth/peft/bitsandbytes are
+absent here, so only this path's time is reported, together with the device
+time the same dequantizations need (hipGraph replay) -- the gap between the two
+is host launch overhead (Python + ctypes + allocation per call).
+
+Also reports the per-call host cost of ``triton_dequantize_nf4`` alone.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from nf4_triton_dequantization import triton_dequantize_nf4  # noqa: E402
+from nf4_triton_dequantization_amd import Linear4bit, dequantize_nf4_many  # noqa: E402
+
+OPTIONS = [(2, 3333, 2048, 8192, 3407, torch.float16),
+           (5, 777, 1024, 4096, 3409, torch.bfloat16),
+           (3, 2048, 4096, 14336, 3408, torch.bfloat16)]
+
+
+class MLP(torch.nn.Module):
+    def __init__(self, hd, m, dtype):
+        super().__init__()
+        self.gate_proj = Linear4bit(hd, m, compute_dtype=dtype).to("cuda")
+        self.up_proj = Linear4bit(hd, m, compute_dtype=dtype).to("cuda")
+        self.down_proj = Linear4bit(m, hd, compute_dtype=dtype).to("cuda")
+
+
+def mlp_dequantize(mlp, fx, sync=True):
+    s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(s1):
+        a = fx(mlp.up_proj).t()
+    with torch.cuda.stream(s2):
+        b = fx(mlp.gate_proj).t()
+    with torch.cuda.stream(s3):
+        c = fx(mlp.down_proj).t()
+    if sync:
+        torch.cuda.synchronize()
+    return a, b, c
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iterations", type=int, default=1000)
+    args = ap.parse_args()
+    total = 0.0
+    for bsz, qlen, hd, m, seed, dt in OPTIONS:
+        torch.manual_seed(seed)
+        mlp = MLP(hd, m, dt)
+        for _ in range(2):
+            mlp_dequantize(mlp, triton_dequantize_nf4)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iterations):
+            mlp_dequantize(mlp, triton_dequantize_nf4, sync=False)
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 1e3
+        total += t
+        # device-only time of the same three dequantizations (graph replay, batched launch)
+        mods = [mlp.up_proj, mlp.gate_proj, mlp.down_proj]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            outs = dequantize_nf4_many(mods)
+        g.replay()
+        torch.cuda.synchronize()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record()
+        for _ in range(50):
+            g.replay()
+        r1.record()
+        torch.cuda.synchronize()
+        dev_us = r0.elapsed_time(r1) * 1e3 / 50
+        elems = 3 * hd * m
+        print(json.dumps({"config": f"hd={hd} m={m} {str(dt).replace('torch.', '')}",
+                          "iterations": args.iterations, "seconds": t, "us_per_iteration": t * 1e6 / args.iterations,
+                          "device_us_per_iteration_batched_graph": dev_us,
+                          "elements_per_iteration": elems}), flush=True)
+        del outs, g
+    # host cost of one API call (device work hidden behind a long queue)
+    lin = Linear4bit(4096, 4096, compute_dtype=torch.bfloat16).to("cuda")
+    for _ in range(20):
+        triton_dequantize_nf4(lin)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)
+    n = 2000
+    t0 = time.perf_counter()
+    for _ in range(n):
+        triton_dequantize_nf4(lin)
+    host_us = (time.perf_counter() - t0) * 1e6 / n
+    torch.cuda.synchronize()
+    print(json.dumps({"reference_style_total_seconds": total, "api_host_us_per_call": host_us}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

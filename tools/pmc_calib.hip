@@ -46,3 +46,31 @@ extern "C" int calib_write(void* p, uint32_t nbytes, void* stream) {
     hipLaunchKernelGGL(calib_write_x4, dim3(2048), dim3(256), 0, (hipStream_t)stream, (uint32_t*)p, nbytes);
     return (int)hipGetLastError();
 }
+
+// Speed-of-light twin of nf4_flat_kernel: the same loads (4 B/lane, 256 B per
+// wave instruction) and the same stores (16 B/lane, 1 KiB per wave instruction,
+// sc1+nt), no decode -- what the memory system gives this access mix.
+__global__ __launch_bounds__(256) void calib_mix(const uint32_t* p, uint32_t nbytes, uint32_t* o) {
+    __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, nbytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)o, 0, nbytes * 4u, 0x00020000);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t base = wave * 1024u; base < nbytes; base += nw * 1024u) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, base + 256u * j + 4u * lane, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const u32x4 v = {w[j], w[j] ^ 1u, w[j] ^ 2u, w[j] ^ 3u};
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, (base + 256u * j + 4u * lane) * 4u, 0, 18);
+        }
+    }
+}
+
+extern "C" int calib_mix_launch(const void* p, uint32_t nbytes, void* o, void* stream) {
+    const uint32_t tiles = (nbytes + 1023u) / 1024u;
+    hipLaunchKernelGGL(calib_mix, dim3((tiles + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const uint32_t*)p, nbytes,
+                       (uint32_t*)o);
+    return (int)hipGetLastError();
+}

@@ -1,0 +1,40 @@
+"""Diagnostics: does the placement of the small absmax arrays change the dequant time?
+
+Compares, in one process (interleaved rounds), 4096^2 and 8192^2 NF4->bf16 over
+rotating packed/output buffers with (a) one shared absmax/nested-absmax pair and
+(b) a separate pair per buffer set (what bench.py does), plus the output-value
+sensitivity check (a2 = rand / tiny / 1 / 0).
+"""
+import ctypes, json, os, sys  # noqa: E401
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "tools")]
+from nf4_triton_dequantization_amd import _lib  # noqa: E402
+from hbm_ceiling import graph_time  # noqa: E402
+
+L = _lib.lib()
+dev = torch.device("cuda", 0)
+for (m, n, P) in ((4096, 4096, 16), (8192, 8192, 8)):
+    nbytes, nb = m * n // 2, m * n // 64
+    n2 = (nb + 255) // 256
+    ins = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=dev) for _ in range(P)]
+    outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(P)]
+    a1s = [torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev) for _ in range(P)]
+    a2s = [torch.rand(n2, device=dev) * 0.01 + 1e-3 for _ in range(P)]
+    variants = {"shared a1/a2": lambda i: (a1s[0], a2s[0]), "per-set a1/a2": lambda i: (a1s[i % P], a2s[i % P]),
+                "per-set a1, shared a2": lambda i: (a1s[i % P], a2s[0]),
+                "shared a1, per-set a2": lambda i: (a1s[0], a2s[i % P])}
+    for r in range(3):
+        for name, pick in variants.items():
+            def deq(i, pick=pick):
+                a1, a2 = pick(i)
+                assert L.nf4_dequant_ref(ins[i % P].data_ptr(), nbytes, a1.data_ptr(), nb, a2.data_ptr(), n2,
+                                         outs[i % P].data_ptr(), _lib.BF16, m, n,
+                                         torch.cuda.current_stream().cuda_stream) == 0
+            t = graph_time(deq, 64)
+            print(json.dumps({"m": m, "round": r, "variant": name, "us": round(t * 1e6, 3),
+                              "TBps": round(nbytes * 5 / t / 1e12, 3)}), flush=True)
+    del ins, outs
+    torch.cuda.empty_cache()
