@@ -75,6 +75,38 @@ def _prepare(module):
     return qweight, absmax, absmax32, dtype, m, n
 
 
+def _flat_ptr(t: torch.Tensor) -> tuple:
+    """(tensor kept alive, data pointer, numel) of a contiguous view; copies only when needed."""
+    if not t.is_contiguous():
+        t = t.contiguous()
+    return t, t.data_ptr(), t.numel()
+
+
+def _launch(qweight, absmax, absmax32, out, m, n, code, stream) -> None:
+    """Casts of kernel_optimized.py:162-186 and one C-ABI call on `stream`."""
+    if qweight.dtype != torch.uint8:
+        qweight = qweight.to(torch.uint8)  # value cast, as :162-163
+    qweight, qp, qn = _flat_ptr(qweight)
+    L = _lib.lib()
+    if absmax.dtype == torch.uint8:
+        if absmax32.dtype != torch.float32:
+            absmax32 = absmax32.to(torch.float32)  # :182
+        absmax, ap, an = _flat_ptr(absmax)
+        absmax32, bp, bn = _flat_ptr(absmax32)
+        if an == 0 or bn == 0:
+            # reference: repeats = ceil(total / 0) -> ZeroDivisionError (:175, :184)
+            raise ZeroDivisionError("integer division or modulo by zero (empty absmax)")
+        rc = L.nf4_dequant_ref(qp, qn, ap, an, bp, bn, out.data_ptr(), code, m, n, stream)
+    else:
+        # single-quant branch (:166-167 -> :273-274): absmax.view(m, -1)[:, :bpr].to(float32)
+        if absmax.dtype != torch.float32:
+            absmax = absmax.to(torch.float32)
+        absmax, ap, an = _flat_ptr(absmax)
+        rc = L.nf4_dequant_single(qp, qn, ap, an, out.data_ptr(), code, m, n, stream)
+    if rc:
+        _lib.check(rc, "nf4 dequantize")
+
+
 def dequantize_nf4_into(qweight: torch.Tensor, absmax: torch.Tensor, absmax32: torch.Tensor,
                         out: torch.Tensor, m: int, n: int) -> torch.Tensor:
     """Dequantize into a caller-provided contiguous ``out`` ([m, n] elements, fp16/bf16/fp32)."""
@@ -84,29 +116,8 @@ def dequantize_nf4_into(qweight: torch.Tensor, absmax: torch.Tensor, absmax32: t
         raise RuntimeError("dequantize_nf4_into: out must be a contiguous tensor of m*n elements")
     if m == 0 or n == 0:
         return out
-    q = _as_u8_flat(qweight)
-    L = _lib.lib()
-    stream = _stream_ptr(q.device)
-    if absmax.dtype == torch.uint8:
-        a1 = absmax.contiguous().view(-1)
-        a2 = absmax32.reshape(-1)
-        if a2.dtype != torch.float32:
-            a2 = a2.to(torch.float32)      # :182
-        a2 = a2.contiguous()
-        if a1.numel() == 0 or a2.numel() == 0:
-            # reference: repeats = ceil(total / 0) -> ZeroDivisionError (:175, :184)
-            raise ZeroDivisionError("integer division or modulo by zero (empty absmax)")
-        rc = L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
-                               out.data_ptr(), code, m, n, stream)
-    else:
-        # single-quant branch (:166-167 -> :273-274): absmax.view(m, -1)[:, :bpr].to(float32)
-        am = absmax.reshape(-1)
-        if am.dtype != torch.float32:
-            am = am.to(torch.float32)
-        am = am.contiguous()
-        rc = L.nf4_dequant_single(q.data_ptr(), q.numel(), am.data_ptr(), am.numel(), out.data_ptr(), code,
-                                  m, n, stream)
-    _lib.check(rc, "nf4 dequantize")
+    with torch.cuda.device(qweight.device):
+        _launch(qweight, absmax, absmax32, out, m, n, code, torch.cuda.current_stream().cuda_stream)
     return out
 
 
@@ -118,13 +129,20 @@ def triton_dequantize_nf4(module) -> torch.Tensor:
     ``quant_state.dtype`` on the weight's device.
     """
     qweight, absmax, absmax32, dtype, m, n = _prepare(module)
-    _require_device(qweight)
-    code_ok = _dtype_code(dtype)  # noqa: F841  -- raise before allocating
-    out = torch.empty((m, n), dtype=dtype, device=qweight.device)
-    if qweight.device.index is not None and qweight.device.index != torch.cuda.current_device():
-        with torch.cuda.device(qweight.device):
-            return dequantize_nf4_into(qweight, absmax, absmax32, out, m, n)
-    return dequantize_nf4_into(qweight, absmax, absmax32, out, m, n)
+    dev = qweight.device
+    if dev.type != "cuda":
+        _require_device(qweight)
+    code = _dtype_code(dtype)  # raise before allocating
+    out = torch.empty((m, n), dtype=dtype, device=dev)
+    if m == 0 or n == 0:
+        return out
+    idx = dev.index
+    if idx is None or idx == torch.cuda.current_device():
+        _launch(qweight, absmax, absmax32, out, m, n, code, torch.cuda.current_stream().cuda_stream)
+    else:
+        with torch.cuda.device(dev):
+            _launch(qweight, absmax, absmax32, out, m, n, code, torch.cuda.current_stream().cuda_stream)
+    return out
 
 
 def reset_triton_dequantize_state() -> None:

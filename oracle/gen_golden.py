@@ -138,6 +138,7 @@ def main():
     manifest = {"generator": "oracle/gen_golden.py",
                 "reference": "nf4_triton_dequantization/kernel_optimized.py:208-314 (_aggressive_pytorch_t4)",
                 "cases": {}}
+    samples = {}
     for big, cases in ((False, SMALL_CASES), (True, BIG_CASES)):
         for name, m, n, dt, seed, ov in cases:
             packed, a1, a2, single = case_inputs(m, n, seed, ov)
@@ -149,8 +150,9 @@ def main():
             if big:
                 rng = np.random.default_rng(seed)
                 idx = np.sort(rng.choice(out.size, size=min(4096, out.size), replace=False))
-                entry["sample_idx"] = idx.tolist()
-                entry["sample_bits"] = out.reshape(-1)[idx].astype(int).tolist()
+                samples[name + "/idx"] = idx.astype(np.int64)
+                samples[name + "/bits"] = out.reshape(-1)[idx]
+                entry["samples"] = "big_samples.npz"
             else:
                 arrays = {"packed": packed, "a1": a1, "a2": a2, "out_bits": out}
                 if ov.get("a2_dtype") == "f16":     # what the path sees after .to(float32) (:182)
@@ -169,6 +171,7 @@ def main():
             k: {"sha256": v, "agrees_with_fallback": v == manifest["cases"][k]["sha256"]} for k, v in got.items()}
         for k, v in manifest["triton_interpret_fp16"].items():
             print(f"triton-interp {k:30s} agrees={v['agrees_with_fallback']}")
+    np.savez_compressed(os.path.join(GOLDEN, "big_samples.npz"), **samples)
     with open(os.path.join(GOLDEN, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
 

@@ -81,3 +81,9 @@ def max_abs_diff(got: np.ndarray, want: np.ndarray, dt: str) -> float:
     a, b = f(got), f(want)
     ok = np.isfinite(a) & np.isfinite(b)
     return float(np.max(np.abs(a[ok] - b[ok]))) if ok.any() else 0.0
+
+
+def big_samples(name: str):
+    """(flat indices, expected bits) sampled from the reference output of a big golden case."""
+    with np.load(os.path.join(GOLDEN, "big_samples.npz"), allow_pickle=False) as z:
+        return z[name + "/idx"], z[name + "/bits"]

@@ -12,8 +12,8 @@ import pytest
 import torch
 
 import nf4_oracle as O
-from _helpers import (DT_CODE, assert_bits_equal, load_case, make_module, max_abs_diff, out_bits, sha,
-                      torch_dtype)
+from _helpers import (DT_CODE, assert_bits_equal, big_samples, load_case, make_module, max_abs_diff, out_bits,
+                      sha, torch_dtype)
 
 pytestmark = pytest.mark.gpu
 
@@ -52,8 +52,8 @@ def test_full_size_matches_reference_digest(manifest, gpu, name):
     p, a1, a2, _ = O.golden_case_inputs(m, n, e["seed"], e["overrides"])
     out = _api().triton_dequantize_nf4(make_module(p, a1, a2, m, n, dt, gpu))
     got = out_bits(out)
-    idx = np.asarray(e["sample_idx"])
-    assert np.array_equal(got.reshape(-1)[idx], np.asarray(e["sample_bits"], dtype=got.dtype)), name
+    idx, bits = big_samples(name)
+    assert np.array_equal(got.reshape(-1)[idx], bits), name
     assert sha(got) == e["sha256"], name
 
 

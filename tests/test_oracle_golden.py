@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import nf4_oracle as O
-from _helpers import DT_CODE, assert_bits_equal, load_case, sha
+from _helpers import DT_CODE, assert_bits_equal, big_samples, load_case, sha
 
 
 def _small(manifest):
@@ -69,8 +69,8 @@ def test_c_oracle_matches_reference_digest_full_size(manifest, coracle, name):
     p, a1, a2, _ = O.golden_case_inputs(e["m"], e["n"], e["seed"], e["overrides"])
     got = coracle.dequant_ref(p, a1, a2, e["m"], e["n"], DT_CODE[e["dtype"]])
     flat = got.reshape(-1)
-    idx = np.asarray(e["sample_idx"])
-    assert np.array_equal(flat[idx], np.asarray(e["sample_bits"], dtype=flat.dtype)), name
+    idx, bits = big_samples(name)
+    assert np.array_equal(flat[idx], bits), name
     assert sha(got) == e["sha256"], name
 
 
