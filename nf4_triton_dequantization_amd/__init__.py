@@ -16,8 +16,9 @@ from .kernel import (  # noqa: F401
     triton_dequantize_nf4,
 )
 from .bnb_layout import Linear4bit, Params4bit, QuantState, quantize_nf4  # noqa: F401
+from .checkpoint import load_nf4_safetensors, save_nf4_safetensors  # noqa: F401
 
 __all__ = ["triton_dequantize_nf4", "reset_triton_dequantize_state", "dequantize_nf4_many",
            "dequantize_nf4_bnb", "dequantize_nf4_into", "Linear4bit", "Params4bit", "QuantState",
-           "quantize_nf4"]
+           "quantize_nf4", "load_nf4_safetensors", "save_nf4_safetensors"]
 __version__ = "0.1.0"
