@@ -125,6 +125,22 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len,
                         void* out, int32_t out_dtype, int64_t m, int64_t n,
                         const nf4_launch_cfg* cfg, void* hip_stream);
 
+/* Fused dequant + GEMM for small M (decode-shaped activations; replaces the
+ * reference harness's `X @ triton_dequantize_nf4(W).t()`, benchmark.py:61-66):
+ *   y[M][N] = x[M][K] . W[N][K]^T,  W = the weights nf4_dequant_ref would
+ *   write (reference semantics, bit-identical), fp32 accumulation (MFMA).
+ * x, y: fp16/bf16 (out_dtype), row-major.  Fast-path shape rules (else
+ * NF4DQ_ERR_SHAPE): M <= NF4DQ_GEMM_MAX_M, N % 64 == 0, K % 128 == 0,
+ * packed_len == N*K/2.  `workspace` must hold nf4_gemm_workspace_bytes(M, N, K)
+ * bytes (0 = none needed) for the split-K partials; the combine is
+ * deterministic (fixed summation order, no atomics). */
+#define NF4DQ_GEMM_MAX_M 32
+size_t nf4_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len,
+                 const uint8_t* absmax_q, int64_t nb, const float* absmax2, int64_t n2,
+                 void* y, int32_t out_dtype, int64_t N, int64_t K,
+                 void* workspace, size_t workspace_bytes, void* hip_stream);
+
 /* Human-readable text for a return code (static storage). */
 const char* nf4_strerror(int code);
 

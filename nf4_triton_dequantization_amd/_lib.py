@@ -28,6 +28,7 @@ ERR_TOO_LARGE = 3
 ERR_HIP_BASE = 1000
 
 BATCH_MAX = 24
+GEMM_MAX_M = 32
 
 
 class MatrixDesc(ctypes.Structure):
@@ -70,6 +71,9 @@ SIGNATURES = {
     "nf4_dequant_bnb_single": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _I64, _I32, _P]),
     "nf4_dequant_ref_cfg": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I32, _I64, _I64,
                                            ctypes.POINTER(LaunchCfg), _P]),
+    "nf4_gemm_workspace_bytes": (ctypes.c_size_t, [_I64, _I64, _I64]),
+    "nf4_gemm_ref": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I32, _I64, _I64, _P, ctypes.c_size_t,
+                                    _P]),
     "nf4_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "nf4_version": (ctypes.c_char_p, []),
 }

@@ -34,36 +34,13 @@
 #include <stdint.h>
 
 #include "../../include/nf4_dequant.h"
+#include "nf4_common.h"
 
 namespace {
 
+using namespace nf4dq;
+
 enum Mode : int { kRef = 0, kSingle = 1, kBnb = 2, kBnbSingle = 3 };
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// Division by a run-time constant for n < 2^31: q = (umulhi(n, mul) + n) >> shift.
-struct FastDiv {
-    uint32_t d, mul, shift;
-};
-
-FastDiv make_fastdiv(uint32_t d) {
-    FastDiv f{d, 0u, 0u};
-    uint32_t s = 0;
-    while (s < 32 && (uint64_t(1) << s) < d) ++s;
-    f.shift = s;
-    f.mul = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << s) - d)) / d + 1);
-    return f;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-    return (__umulhi(n, f.mul) + n) >> f.shift;
-}
-__device__ __forceinline__ uint32_t fmodu(uint32_t n, const FastDiv& f) {
-    return n - fdiv(n, f) * f.d;
-}
 
 // Kernel-argument image of one matrix on the flat path.
 struct Desc {
@@ -91,28 +68,6 @@ struct Batch {
     uint32_t seg_shift;  // tiles are split into 2^seg_shift contiguous segments, one per block residue
 };
 
-// Keep an fp32 product opaque to the backend: without this, hipcc folds
-// fptrunc(fmul) into v_fma_mix*_f16(a, b, +0), which rounds once instead of
-// twice (fp32 product, then fp16 -- the reference's order) and turns -0 into +0.
-__device__ __forceinline__ float opaque(float x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-
-template <int DT>
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-    if constexpr (DT == NF4DQ_F16) {
-        lo = opaque(lo);
-        hi = opaque(hi);
-    }
-    f32x2 v = {lo, hi};
-    if constexpr (DT == NF4DQ_BF16) {
-        return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
-    } else {
-        return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
-    }
-}
-
 // Scalar store of one output element (rows kernels).
 template <int DT>
 __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
@@ -125,26 +80,6 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
     }
 }
 
-// Scale of flat block g (reference rules in the header of oracle/nf4_oracle.c).
-template <int MODE>
-__device__ __forceinline__ float block_scale(const Desc& D, uint32_t g) {
-    if constexpr (MODE == kRef) {
-        const float q = (float)D.a1[fmodu(g, D.nb)];
-        const uint32_t r = fdiv(g, D.bpr);
-        const uint32_t b = g - r * D.bpr.d;
-        const float s2 = D.a2[fmodu(r * D.groups + (b >> 2), D.n2)];
-        return (q / 127.0f) * s2;  // IEEE division (:45, :270), then fp32 multiply
-    } else if constexpr (MODE == kSingle) {
-        const uint32_t r = fdiv(g, D.bpr);
-        const uint32_t b = g - r * D.bpr.d;
-        return D.a2[r * D.n2.d + b];
-    } else if constexpr (MODE == kBnb) {
-        return D.code2[D.a1[g]] * D.a2[g >> D.blk2_shift] + D.offset;
-    } else {
-        return D.a2[g];
-    }
-}
-
 constexpr int kWg = 256;  // 4 waves (rows / bytes kernels; the flat kernel takes WPG)
 
 // Cache-policy bits of the buffer instructions (aux operand, gfx950 CPol):
@@ -153,7 +88,6 @@ constexpr int kWg = 256;  // 4 waves (rows / bytes kernels; the flat kernel take
 // than nt alone and a cheaper end-of-kernel write-back).
 constexpr int kAuxNt = 2;
 constexpr int kAuxStore = 18;
-constexpr int kRsrcFlags = 0x00020000;  // raw buffer, dword format (gfx950)
 
 template <int DT>
 constexpr uint32_t out_bytes_per_packed_byte() { return DT == NF4DQ_F32 ? 8u : 4u; }
@@ -283,19 +217,6 @@ __device__ __forceinline__ uint32_t find_matrix(const Batch<MAXB>& bt, uint32_t 
         while (k + 1 < bt.count && t >= bt.d[k + 1].tile_begin) ++k;
     }
     return k;
-}
-
-// The 16 NF4 code points (fp32 bit patterns of kernel_optimized.py:234-239)
-// into LDS from immediates (no global load on the
-// kernel's critical path): thread 0 writes four 16-byte rows.
-__device__ __forceinline__ void write_lut(float* lut) {
-    if (threadIdx.x == 0) {
-        u32x4* l4 = reinterpret_cast<u32x4*>(lut);
-        l4[0] = u32x4{0xbf800000u, 0xbf3239b1u, 0xbf066b30u, 0xbeca32a0u};
-        l4[1] = u32x4{0xbe91a24du, 0xbe3d353fu, 0xbdba7871u, 0x00000000u};
-        l4[2] = u32x4{0x3da2faffu, 0x3e24cae3u, 0x3e7c04ddu, 0x3ead033au};
-        l4[3] = u32x4{0x3ee1a4b8u, 0x3f1007abu, 0x3f3913b3u, 0x3f800000u};
-    }
 }
 
 // Position of a wave in the launch: the i-th tile of its segment, which is

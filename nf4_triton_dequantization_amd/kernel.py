@@ -233,3 +233,55 @@ def dequantize_nf4_bnb(module) -> torch.Tensor:
                                       bs, stream)
     _lib.check(rc, "nf4 bnb dequantize")
     return out
+
+
+def nf4_linear(x: torch.Tensor, module, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x @ W.t() (+ bias)`` for an NF4 ``Linear4bit`` weight W (reference semantics).
+
+    The consumer of the reference harness (benchmark.py:61-66,
+    ``X @ triton_dequantize_nf4(W).t()``).  Decode-shaped inputs (at most
+    ``NF4DQ_GEMM_MAX_M`` rows, N % 64 == 0, K % 128 == 0, uint8 absmax) run the
+    fused kernel: the 4-bit weight is read once and dequantized in registers
+    into exactly the bf16/fp16 values ``triton_dequantize_nf4`` returns, then
+    multiplied on MFMA with fp32 accumulation.  Anything else dequantizes with
+    the HIP kernel and multiplies with torch (hipBLASLt).  Output dtype =
+    ``quant_state.dtype``; ``x`` is cast to it first, as the reference harness's
+    inputs already are.
+    """
+    qweight, absmax, absmax32, dtype, m, n = _prepare(module)
+    _require_device(qweight)
+    N, K = m, n
+    if x.shape[-1] != K:
+        raise RuntimeError(f"nf4_linear: x has {x.shape[-1]} features, weight expects {K}")
+    lead = x.shape[:-1]
+    M = x.numel() // K if K else 0
+    fused = (dtype in (torch.float16, torch.bfloat16) and absmax.dtype == torch.uint8 and 0 < M <= _lib.GEMM_MAX_M
+             and N % 64 == 0 and K % 128 == 0 and qweight.numel() * qweight.element_size() == N * K // 2
+             and qweight.dtype == torch.uint8)
+    if not fused:
+        w = triton_dequantize_nf4(module)
+        y = x.to(dtype) @ w.t()
+    else:
+        xc = x.reshape(M, K)
+        if xc.dtype != dtype:
+            xc = xc.to(dtype)
+        xc = xc.contiguous()
+        y = torch.empty((M, N), dtype=dtype, device=qweight.device)
+        L = _lib.lib()
+        ws_bytes = L.nf4_gemm_workspace_bytes(M, N, K)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=qweight.device) if ws_bytes else None
+        with torch.cuda.device(qweight.device):
+            q, qp, qn = _flat_ptr(qweight)
+            a1, ap, an = _flat_ptr(absmax)
+            a2 = absmax32 if absmax32.dtype == torch.float32 else absmax32.to(torch.float32)
+            a2, bp, bn = _flat_ptr(a2)
+            if an == 0 or bn == 0:
+                raise ZeroDivisionError("integer division or modulo by zero (empty absmax)")
+            rc = L.nf4_gemm_ref(xc.data_ptr(), M, qp, qn, ap, an, bp, bn, y.data_ptr(), _dtype_code(dtype), N, K,
+                                ws.data_ptr() if ws is not None else None, ws_bytes,
+                                torch.cuda.current_stream().cuda_stream)
+        _lib.check(rc, "nf4 fused gemm")
+        y = y.reshape(*lead, N)
+    if bias is not None:
+        y = y + bias.to(y.dtype)
+    return y.reshape(*lead, N)

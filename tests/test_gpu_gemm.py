@@ -1,0 +1,113 @@
+"""Fused NF4 dequant-GEMM (``nf4_linear`` / ``nf4_gemm_ref``) vs a float64 oracle (``-m gpu``).
+
+Oracle: W = the reference's dequantized weights from the C oracle (bit-exact
+bf16/fp16, pinned to the reference fallback), X the same fp16/bf16 inputs, the
+product in float64.  Tolerance (written here): fp32 accumulation of K terms
+plus one final rounding to the output dtype,
+    |y - ref| <= 2^-p |ref| + 2^-20 * sum_k |x_k w_k|,   p = 8 (bf16), 10 (fp16).
+"""
+import numpy as np
+import pytest
+import torch
+
+import nf4_oracle as O
+from _helpers import make_module
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits_to_f64(bits, dt):
+    if dt == "f16":
+        return bits.view(np.float16).astype(np.float64)
+    return (bits.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+
+
+def _check(y, x_bits, w_bits, dt):
+    xf = _bits_to_f64(x_bits, dt)
+    wf = _bits_to_f64(w_bits, dt)
+    ref = xf @ wf.T
+    mag = np.abs(xf) @ np.abs(wf).T
+    p = 8 if dt == "bf16" else 10
+    tol = 2.0 ** -p * np.abs(ref) + 2.0 ** -20 * mag
+    yb = y.contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+    got = _bits_to_f64(yb, dt).reshape(ref.shape)
+    bad = np.abs(got - ref) > tol
+    assert not bad.any(), f"{bad.sum()} of {bad.size} outside tolerance; worst {np.abs(got - ref).max():.3g}"
+
+
+def _x_bits(M, K, dt, seed):
+    x = O.normal_f32(seed, M * K, stream=9).reshape(M, K)
+    t = torch.from_numpy(x).to(torch.float16 if dt == "f16" else torch.bfloat16)
+    return t, t.view(torch.int16).numpy().view(np.uint16)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,N,K", [(1, 64, 128), (3, 128, 512), (16, 256, 1024), (17, 192, 384), (32, 64, 4096),
+                                   (1, 4096, 4096), (8, 1024, 4096), (4, 512, 11008), (2, 448, 14336)])
+def test_fused_gemm_vs_float64_oracle(coracle, gpu, dt, M, N, K):
+    from nf4_triton_dequantization_amd import nf4_linear
+
+    packed, a1, a2 = O.make_inputs(N, K, seed=M * 7 + N + K, a2_kind="normal")
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16)
+    mod = make_module(packed, a1, a2, N, K, dt, gpu)
+    xt, xb = _x_bits(M, K, dt, seed=M + K)
+    y = nf4_linear(xt.to(gpu), mod)
+    assert y.shape == (M, N) and y.dtype == xt.dtype
+    _check(y, xb, W, dt)
+
+
+def test_fused_matches_unfused_composite(gpu):
+    """Same inputs through the fused kernel and through dequant + torch matmul."""
+    from nf4_triton_dequantization import triton_dequantize_nf4
+    from nf4_triton_dequantization_amd import nf4_linear
+
+    packed, a1, a2 = O.make_inputs(1024, 4096, seed=5)
+    mod = make_module(packed, a1, a2, 1024, 4096, "bf16", gpu)
+    xt, _ = _x_bits(4, 4096, "bf16", seed=6)
+    x = xt.to(gpu)
+    y1 = nf4_linear(x, mod).float()
+    y2 = (x.float() @ triton_dequantize_nf4(mod).float().t())
+    assert torch.allclose(y1, y2, rtol=2 ** -7, atol=1e-2 * y2.abs().max().item())
+
+
+def test_wrapping_absmax_and_leading_dims(coracle, gpu):
+    """nb / n2 wrap (reference repeat semantics) and a [batch, seq, K] input."""
+    from nf4_triton_dequantization_amd import nf4_linear
+
+    N, K = 128, 256
+    packed, a1, a2, _ = O.golden_case_inputs(N, K, 12, {"nb": 7, "n2": 3})
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16)
+    mod = make_module(packed, a1, a2, N, K, "bf16", gpu)
+    xt, xb = _x_bits(6, K, "bf16", seed=13)
+    y = nf4_linear(xt.to(gpu).reshape(2, 3, K), mod)
+    assert y.shape == (2, 3, N)
+    _check(y.reshape(6, N), xb, W, "bf16")
+
+
+def test_large_m_takes_composite_path(coracle, gpu):
+    from nf4_triton_dequantization_amd import nf4_linear
+
+    N, K, M = 256, 512, 80
+    packed, a1, a2 = O.make_inputs(N, K, seed=21)
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16)
+    mod = make_module(packed, a1, a2, N, K, "bf16", gpu)
+    xt, xb = _x_bits(M, K, "bf16", seed=22)
+    bias = torch.randn(N, device=gpu).to(torch.bfloat16)
+    y = nf4_linear(xt.to(gpu), mod, bias=bias)
+    y0 = nf4_linear(xt.to(gpu), mod)
+    _check(y0, xb, W, "bf16")
+    assert torch.allclose((y - y0).float(), bias.float().expand(M, N), atol=0.05)
+
+
+def test_abi_rejects_non_fast_shapes(gpu):
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    F = 0x1000
+    assert L.nf4_gemm_ref(F, 33, F, 64 * 64, F, 64, F, 1, F, _lib.BF16, 64, 128, None, 0, None) == _lib.ERR_SHAPE
+    assert L.nf4_gemm_ref(F, 1, F, 32 * 64, F, 64, F, 1, F, _lib.BF16, 32, 128, None, 0, None) == _lib.ERR_SHAPE
+    assert L.nf4_gemm_ref(F, 1, F, 64 * 48, F, 64, F, 1, F, _lib.BF16, 64, 96, None, 0, None) == _lib.ERR_SHAPE
+    assert L.nf4_gemm_ref(F, 1, F, 64 * 64, F, 64, F, 1, F, _lib.F32, 64, 128, None, 0, None) == _lib.ERR_ARG
+    need = L.nf4_gemm_workspace_bytes(1, 4096, 4096)
+    assert need > 0
+    assert L.nf4_gemm_ref(F, 1, F, 4096 * 2048, F, 64, F, 1, F, _lib.BF16, 4096, 4096, None, 0, None) == _lib.ERR_ARG
