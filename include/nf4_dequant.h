@@ -131,9 +131,12 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len,
  *   write (reference semantics, bit-identical), fp32 accumulation (MFMA).
  * x, y: fp16/bf16 (out_dtype), row-major.  Fast-path shape rules (else
  * NF4DQ_ERR_SHAPE): M <= NF4DQ_GEMM_MAX_M, N % 64 == 0, K % 128 == 0,
- * packed_len == N*K/2.  `workspace` must hold nf4_gemm_workspace_bytes(M, N, K)
- * bytes (0 = none needed) for the split-K partials; the combine is
- * deterministic (fixed summation order, no atomics). */
+ * packed_len == N*K/2 (and N <= 2^18).  `workspace` (16-byte aligned) must hold
+ * nf4_gemm_workspace_bytes(M, N, K) bytes (0 = none needed): split-K ticket
+ * counters + fp32 partials, reduced inside the launch in a fixed order
+ * (bitwise reproducible).  The workspace must be ZERO-FILLED before its first
+ * use; every call leaves it reusable (counters back to 0).  One workspace per
+ * stream: concurrent calls must not share one. */
 #define NF4DQ_GEMM_MAX_M 32
 size_t nf4_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len,

@@ -18,8 +18,9 @@
 // lane's 32) and activation bytes [16s, 16s+16) its A fragment -- the same k
 // permutation on both operands, so no shuffle is needed.  Chunks are
 // software-pipelined two deep (register sets P/Q).  K slices > 1 write fp32
-// partials to a workspace slab, summed in a fixed order by a second kernel
-// (bitwise reproducible; no atomics).
+// partials to a workspace slab; the last workgroup to finish a column group
+// (ticket counter) sums the slices in slice order and writes y -- one launch,
+// bitwise reproducible, no float atomics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -34,7 +35,17 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kGemmWaves = 4;
+constexpr int kGemmWaves = 8;
+constexpr int kAuxSc1 = 16;  // write-through stores / L2-bypassing loads (cross-XCD hand-off)
+
+template <int DT>
+__device__ __forceinline__ void store_y(void* y, uint32_t i, float v) {
+    if constexpr (DT == NF4DQ_BF16) {
+        reinterpret_cast<__bf16*>(y)[i] = (__bf16)v;
+    } else {
+        reinterpret_cast<_Float16*>(y)[i] = (_Float16)opaque(v);
+    }
+}
 constexpr uint32_t kChunkK = 128;
 
 struct GemmArgs {
@@ -44,8 +55,9 @@ struct GemmArgs {
     const void* x;          // [M][K] fp16/bf16
     void* y;                // [M][N] fp16/bf16
     float* slab;            // [ksplit][M][N] fp32 partials (ksplit > 1)
+    uint32_t* counters;     // [N / 64] split-K tickets, 0 between calls
     uint32_t M, N, K;
-    uint32_t col_groups;    // N / 64
+    uint32_t col_groups;    // N / 16 column strips
     uint32_t ksplit;
     uint32_t chunks_per_split;
     uint32_t chunks;        // K / 128
@@ -53,49 +65,43 @@ struct GemmArgs {
     FastDiv nb, n2;
 };
 
+// One 128-deep K chunk of one lane: 16 packed weight bytes of its row (one
+// 64-block, so one scale) and MT x 4 activation fragments.
 template <int MT>
 struct Chunk {
-    u32x4 w;          // 16 packed bytes = 32 weights of this lane's row
-    uint32_t a1;      // absmax byte of the lane's 64-block
-    float a2;         // nested absmax of the lane's 256-group
-    u32x4 x[MT][4];   // activation fragments: M-tile mt, MFMA step s
+    u32x4 w;
+    uint32_t qa;    // absmax byte
+    float qb;       // nested absmax
+    u32x4 x[MT][4];
 };
 
 template <int MT>
-__device__ __forceinline__ Chunk<MT> chunk_load(const GemmArgs& A, __amdgpu_buffer_rsrc_t rw,
-                                                __amdgpu_buffer_rsrc_t rx, uint32_t c, bool valid, uint32_t row,
-                                                uint32_t nl, uint32_t kh) {
-    Chunk<MT> in;
+__device__ __forceinline__ void chunk_issue(const GemmArgs& A, __amdgpu_buffer_rsrc_t rw, __amdgpu_buffer_rsrc_t rx,
+                                            uint32_t c, bool valid, uint32_t row, uint32_t nl, uint32_t kh,
+                                            Chunk<MT>& in) {
     const uint32_t kbase = c * kChunkK + 32u * kh;
-    // past the last chunk: offsets beyond the buffer ranges (zeros, no traffic)
-    const uint32_t woff = valid ? row * (A.K >> 1) + (kbase >> 1) : 0xFFFFFFF0u;
-    in.w = __builtin_amdgcn_raw_buffer_load_b128(rw, woff, 0, 0);
-    const uint32_t cc = valid ? c : 0u;
-    const uint32_t b = 2u * cc + (kh >> 1);                 // 64-block of the lane within its row
-    in.a1 = A.a1[fmodu(row * A.bpr + b, A.nb)];               // (:173-177 wrap)
-    in.a2 = A.a2[fmodu(row * A.groups + (b >> 2), A.n2)];    // (:40-41, :183-186 wrap)
+    // past the wave's last chunk: offsets beyond the buffer ranges (zeros, no traffic)
+    in.w = __builtin_amdgcn_raw_buffer_load_b128(rw, valid ? row * (A.K >> 1) + (kbase >> 1) : 0xFFFFFFF0u, 0, 0);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-        const uint32_t xrow = 16u * mt + nl;  // rows >= M fall outside the buffer: zeros
-        const uint32_t xoff = valid ? (xrow * A.K + kbase) * 2u : 0xFFFFFF00u;
+        const uint32_t xoff = valid ? ((16u * mt + nl) * A.K + kbase) * 2u : 0xFFFFFF00u;  // rows >= M: zeros
 #pragma unroll
         for (int s = 0; s < 4; ++s) in.x[mt][s] = __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + 16u * s, 0, 0);
     }
-    return in;
+    const uint32_t b = 2u * (valid ? c : 0u) + (kh >> 1);  // 64-block within the row
+    in.qa = A.a1[fmodu(row * A.bpr + b, A.nb)];               // (:173-177 wrap)
+    in.qb = A.a2[fmodu(row * A.groups + (b >> 2), A.n2)];    // (:40-41, :183-186 wrap)
 }
 
 template <int DT, int MT>
 __device__ __forceinline__ void chunk_mma(const Chunk<MT>& in, const float* lut, f32x4 (&acc)[MT]) {
-    // keep this chunk's math below the next chunk's loads: hipcc otherwise
-    // hoists the scale division next to the loads and waits vmcnt(0) on them
-    __builtin_amdgcn_sched_barrier(0);
-    const float sc = ((float)in.a1 / 127.0f) * in.a2;  // IEEE division, then fp32 multiply (:45)
+    const float sc = ((float)in.qa / 127.0f) * in.qb;  // IEEE division, then fp32 multiply (:45)
     const char* t = reinterpret_cast<const char*>(lut);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-        const uint32_t w = in.w[s];
-        const uint32_t hi4 = (w >> 2) & 0x3C3C3C3Cu;
-        const uint32_t lo4 = (w << 2) & 0x3C3C3C3Cu;
+        const uint32_t wd = in.w[s];
+        const uint32_t hi4 = (wd >> 2) & 0x3C3C3C3Cu;
+        const uint32_t lo4 = (wd << 2) & 0x3C3C3C3Cu;
         float v[8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -118,83 +124,117 @@ __device__ __forceinline__ void chunk_mma(const Chunk<MT>& in, const float* lut,
     }
 }
 
-template <int DT, int MT>
+// Workgroup = kGemmWaves waves owning 16 output columns of one K slice; wave
+// w takes every kGemmWaves-th group of D chunks, D chunks in flight at a time;
+// the waves' partial sums are combined through LDS (fixed order).
+template <int DT, int MT, int D>
 __global__ __launch_bounds__(64 * kGemmWaves) void nf4_gemm_smallm_kernel(const GemmArgs A) {
-    __shared__ __attribute__((aligned(16))) float lut[16];
+    __shared__ __attribute__((aligned(16))) float lut[20];  // 16 codes + the last-arriver flag
+    __shared__ __attribute__((aligned(16))) f32x4 red[kGemmWaves][MT][64];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t nl = lane & 15u, kh = lane >> 4;
-    const uint32_t cg = blockIdx.x % A.col_groups;
-    const uint32_t ks = blockIdx.x / A.col_groups;
-    const uint32_t n0 = (cg * kGemmWaves + wave) * 16u;
-    const uint32_t row = n0 + nl;
+    const uint32_t cg = blockIdx.x % A.col_groups;   // 16-column strip
+    const uint32_t ks = blockIdx.x / A.col_groups;   // K slice
+    const uint32_t row = cg * 16u + nl;
     const uint32_t c0 = ks * A.chunks_per_split;
     const uint32_t c1 = c0 + A.chunks_per_split < A.chunks ? c0 + A.chunks_per_split : A.chunks;
 
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.N * (A.K >> 1), kRsrcFlags);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
 
-    Chunk<MT> P = chunk_load<MT>(A, rw, rx, c0, c0 < c1, row, nl, kh);
-    write_lut(lut);
-    __syncthreads();
-
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (uint32_t c = c0; c < c1; c += 2) {
-        const Chunk<MT> Q = chunk_load<MT>(A, rw, rx, c + 1, c + 1 < c1, row, nl, kh);
-        chunk_mma<DT, MT>(P, lut, acc);
-        if (c + 1 >= c1) break;
-        P = chunk_load<MT>(A, rw, rx, c + 2, c + 2 < c1, row, nl, kh);
-        chunk_mma<DT, MT>(Q, lut, acc);
+    bool first = true;
+    for (uint32_t g = c0 + wave * D; g < c1 || first; g += kGemmWaves * D) {
+        Chunk<MT> ch[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) chunk_issue<MT>(A, rw, rx, g + d, g + d < c1, row, nl, kh, ch[d]);
+        if (first) {  // LUT + barrier overlap the first loads
+            write_lut(lut);
+            __syncthreads();
+            first = false;
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) chunk_mma<DT, MT>(ch[d], lut, acc);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[mt];
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        f32x4 s = red[0][mt][lane];
+#pragma unroll
+        for (int w = 1; w < kGemmWaves; ++w) s += red[w][mt][lane];
+        acc[mt] = s;
     }
 
     // acc[mt][r] = Y[16 mt + 4 kh + r][n0 + nl]
+    if (A.ksplit == 1) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t m = 16u * mt + 4u * kh + r;
+                if (m < A.M) store_y<DT>(A.y, m * A.N + row, acc[mt][r]);
+            }
+        }
+        return;
+    }
+
+    // Split-K, reduced inside the launch (MI355X_MICROARCH.md / cdna guide G16,
+    // write-through form): every slice writes its fp32 partials with sc1
+    // stores, drains them, and one lane per workgroup takes a ticket on the
+    // column group's counter; the workgroup drawing ksplit-1 sums all slices
+    // in slice order (sc1 loads: no stale line from any L2), writes y, and
+    // resets the counter to 0 for the next call.  Bitwise reproducible.
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)A.slab, 0, A.ksplit * A.M * A.N * 4u, kRsrcFlags);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t m = 16u * mt + 4u * kh + r;
-            if (m < A.M) {
-                if (A.ksplit == 1) {
-                    if constexpr (DT == NF4DQ_BF16) {
-                        reinterpret_cast<__bf16*>(A.y)[m * A.N + row] = (__bf16)acc[mt][r];
-                    } else {
-                        reinterpret_cast<_Float16*>(A.y)[m * A.N + row] = (_Float16)opaque(acc[mt][r]);
-                    }
-                } else {
-                    A.slab[(ks * A.M + m) * A.N + row] = acc[mt][r];
-                }
-            }
+            const uint32_t off = m < A.M ? ((ks * A.M + m) * A.N + row) * 4u : 0xFFFFFFF0u;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][r]), rs, off, 0, kAuxSc1);
         }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // only wave 0 is left: its own drain is the hand-off
+    uint32_t last = 0;
+    if (lane == 0) {
+        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[cg], 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        last = ticket == A.ksplit - 1u;
+        if (last) __hip_atomic_store(&A.counters[cg], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last = __builtin_amdgcn_readfirstlane(last);
+    if (!last) return;
+    for (uint32_t i = lane; i < A.M * 16u; i += 64u) {
+        const uint32_t m = i >> 4;
+        const uint32_t n = cg * 16u + (i & 15u);
+        float sum = 0.0f;
+        for (uint32_t k = 0; k < A.ksplit; ++k) {
+            sum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ((k * A.M + m) * A.N + n) * 4u, 0,
+                                                                        kAuxSc1));
+        }
+        store_y<DT>(A.y, m * A.N + n, sum);
     }
 }
 
-// Y = RNE(sum over K slices, slice order fixed) -- deterministic split-K combine.
-template <int DT>
-__global__ __launch_bounds__(256) void nf4_gemm_combine_kernel(const float* slab, void* y, uint32_t MN,
-                                                               uint32_t ksplit) {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < MN; i += gridDim.x * 256u) {
-        float s = slab[i];
-        for (uint32_t k = 1; k < ksplit; ++k) s += slab[k * MN + i];
-        if constexpr (DT == NF4DQ_BF16) {
-            reinterpret_cast<__bf16*>(y)[i] = (__bf16)s;
-        } else {
-            reinterpret_cast<_Float16*>(y)[i] = (_Float16)opaque(s);
-        }
-    }
-}
-
-// K slices: enough waves to cover the chip (~4096), at least 4 chunks per slice.
-uint32_t choose_ksplit(int64_t N, int64_t K) {
-    const int64_t strips = N / 16;
-    const int64_t chunks = K / kChunkK;
-    int64_t ks = (4096 + strips - 1) / strips;
-    const int64_t max_ks = chunks / 4 > 0 ? chunks / 4 : 1;
+// K split across workgroups only when there are too few 16-column strips to
+// give every CU two workgroups; each slice keeps >= kGemmWaves chunks.
+uint32_t choose_ksplit(int64_t M, int64_t N, int64_t K) {
+    (void)M;
+    const int64_t strips = N / 16, chunks = K / kChunkK;
+    int64_t ks = (512 + strips - 1) / strips;
+    const int64_t max_ks = chunks / kGemmWaves > 0 ? chunks / kGemmWaves : 1;
     if (ks > max_ks) ks = max_ks;
-    if (ks < 1) ks = 1;
-    return (uint32_t)ks;
+    return (uint32_t)(ks < 1 ? 1 : ks);
 }
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 inline int hip_rc2(hipError_t e) { return e == hipSuccess ? NF4DQ_OK : NF4DQ_ERR_HIP_BASE + (int)e; }
 
@@ -202,10 +242,16 @@ inline int hip_rc2(hipError_t e) { return e == hipSuccess ? NF4DQ_OK : NF4DQ_ERR
 
 extern "C" {
 
+// Workspace: [64 KiB of uint32 ticket counters][ksplit * M * N fp32 partials].
+// The counter region has a fixed size so that no call's partials ever overlay
+// another call's counters (those must stay 0 between calls): N <= 2^18.
+constexpr size_t kCounterBytes = 64 * 1024;
+static size_t counters_bytes(int64_t) { return kCounterBytes; }
+
 size_t nf4_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
     if (M <= 0 || N <= 0 || K <= 0 || N % 64 || K % kChunkK) return 0;
-    const uint32_t ks = choose_ksplit(N, K);
-    return ks > 1 ? (size_t)ks * (size_t)M * (size_t)N * sizeof(float) : 0;
+    const uint32_t ks = choose_ksplit(M, N, K);
+    return ks > 1 ? counters_bytes(N) + (size_t)ks * (size_t)M * (size_t)N * sizeof(float) : 0;
 }
 
 int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,
@@ -217,21 +263,23 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
     if (M == 0 || N == 0) return NF4DQ_OK;
     if (!x || !packed || !absmax_q || !absmax2 || !y) return NF4DQ_ERR_ARG;
     if (M > NF4DQ_GEMM_MAX_M || N % 64 || K % kChunkK || packed_len != N * (K / 2)) return NF4DQ_ERR_SHAPE;
+    if ((size_t)(N / 16) * 4 > kCounterBytes) return NF4DQ_ERR_TOO_LARGE;
     if (packed_len >= (int64_t(1) << 31) || M * K * 2 >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
-    const uint32_t ks = choose_ksplit(N, K);
-    const size_t need = ks > 1 ? (size_t)ks * (size_t)M * (size_t)N * sizeof(float) : 0;
-    if (need && (!workspace || workspace_bytes < need)) return NF4DQ_ERR_ARG;
+    const uint32_t ks = choose_ksplit(M, N, K);
+    const size_t need = nf4_gemm_workspace_bytes(M, N, K);
+    if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
     GemmArgs A{};
     A.packed = packed;
     A.a1 = absmax_q;
     A.a2 = absmax2;
     A.x = x;
     A.y = y;
-    A.slab = reinterpret_cast<float*>(workspace);
+    A.counters = reinterpret_cast<uint32_t*>(workspace);
+    A.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + counters_bytes(N)) : nullptr;
     A.M = (uint32_t)M;
     A.N = (uint32_t)N;
     A.K = (uint32_t)K;
-    A.col_groups = (uint32_t)(N / 64);
+    A.col_groups = (uint32_t)(N / 16);
     A.ksplit = ks;
     A.chunks = (uint32_t)(K / kChunkK);
     A.chunks_per_split = (A.chunks + ks - 1) / ks;
@@ -241,24 +289,16 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
     A.n2 = make_fastdiv((uint32_t)(n2 > (int64_t(1) << 31) ? (int64_t(1) << 31) : n2));
     const dim3 grid(A.col_groups * ks), block(64 * kGemmWaves);
     const int mt = (int)((M + 15) / 16);
-#define NF4_G(DT_, MT_) hipLaunchKernelGGL((nf4_gemm_smallm_kernel<DT_, MT_>), grid, block, 0, st, A)
-    if (dtype == NF4DQ_BF16) {
-        if (mt == 1) NF4_G(NF4DQ_BF16, 1);
-        else NF4_G(NF4DQ_BF16, 2);
-    } else {
-        if (mt == 1) NF4_G(NF4DQ_F16, 1);
-        else NF4_G(NF4DQ_F16, 2);
-    }
+#define NF4_G(DT_, MT_, D_) hipLaunchKernelGGL((nf4_gemm_smallm_kernel<DT_, MT_, D_>), grid, block, 0, st, A)
+#define NF4_S(DT_)                          \
+    do {                                    \
+        if (mt == 1) NF4_G(DT_, 1, 4);      \
+        else NF4_G(DT_, 2, 2);              \
+    } while (0)
+    if (dtype == NF4DQ_BF16) NF4_S(NF4DQ_BF16);
+    else NF4_S(NF4DQ_F16);
+#undef NF4_S
 #undef NF4_G
-    if (ks > 1) {
-        const uint32_t MN = (uint32_t)(M * N);
-        uint32_t g = (MN + 255) / 256;
-        if (g > 4096) g = 4096;
-        if (dtype == NF4DQ_BF16)
-            hipLaunchKernelGGL((nf4_gemm_combine_kernel<NF4DQ_BF16>), dim3(g), dim3(256), 0, st, A.slab, y, MN, ks);
-        else
-            hipLaunchKernelGGL((nf4_gemm_combine_kernel<NF4DQ_F16>), dim3(g), dim3(256), 0, st, A.slab, y, MN, ks);
-    }
     return hip_rc2(hipGetLastError());
 }
 

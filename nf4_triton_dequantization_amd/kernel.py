@@ -235,6 +235,24 @@ def dequantize_nf4_bnb(module) -> torch.Tensor:
     return out
 
 
+_GEMM_WS = {}
+
+
+def _gemm_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """Zero-filled split-K workspace, one per (device, stream), grown on demand.
+
+    The fused kernel leaves its ticket counters at 0 after every call, so the
+    buffer stays valid; a new stream gets its own (calls on different streams
+    may run concurrently and must not share counters).
+    """
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _GEMM_WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
+        _GEMM_WS[key] = ws
+    return ws
+
+
 def nf4_linear(x: torch.Tensor, module, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``x @ W.t() (+ bias)`` for an NF4 ``Linear4bit`` weight W (reference semantics).
 
@@ -269,8 +287,8 @@ def nf4_linear(x: torch.Tensor, module, bias: Optional[torch.Tensor] = None) -> 
         y = torch.empty((M, N), dtype=dtype, device=qweight.device)
         L = _lib.lib()
         ws_bytes = L.nf4_gemm_workspace_bytes(M, N, K)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=qweight.device) if ws_bytes else None
         with torch.cuda.device(qweight.device):
+            ws = _gemm_workspace(qweight.device, ws_bytes) if ws_bytes else None
             q, qp, qn = _flat_ptr(qweight)
             a1, ap, an = _flat_ptr(absmax)
             a2 = absmax32 if absmax32.dtype == torch.float32 else absmax32.to(torch.float32)

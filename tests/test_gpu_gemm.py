@@ -111,3 +111,15 @@ def test_abi_rejects_non_fast_shapes(gpu):
     need = L.nf4_gemm_workspace_bytes(1, 4096, 4096)
     assert need > 0
     assert L.nf4_gemm_ref(F, 1, F, 4096 * 2048, F, 64, F, 1, F, _lib.BF16, 4096, 4096, None, 0, None) == _lib.ERR_ARG
+
+
+def test_workspace_reuse_across_shapes(coracle, gpu):
+    """Calls of different N / split-K share one workspace; counters stay consistent."""
+    from nf4_triton_dequantization_amd import nf4_linear
+
+    for (M, N, K) in [(8, 1024, 4096), (1, 4096, 4096), (2, 64, 4096), (1, 4096, 4096), (4, 2048, 8192)] * 2:
+        packed, a1, a2 = O.make_inputs(N, K, seed=N + K + M)
+        W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16)
+        mod = make_module(packed, a1, a2, N, K, "bf16", gpu)
+        xt, xb = _x_bits(M, K, "bf16", seed=M + 1)
+        _check(nf4_linear(xt.to(gpu), mod), xb, W, "bf16")

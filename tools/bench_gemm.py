@@ -83,7 +83,7 @@ def main():
         xs = {k: torch.randn((M, k), device=dev).to(torch.bfloat16) for k in {k for _, k in SHAPES}}
         ys = [torch.empty((M, n), dtype=torch.bfloat16, device=dev) for (n, _, _, _, _) in ws]
         wsz = max(L.nf4_gemm_workspace_bytes(M, n, k) for (n, k) in SHAPES)
-        work = torch.empty(max(wsz, 1), dtype=torch.uint8, device=dev)
+        work = torch.zeros(max(wsz, 1), dtype=torch.uint8, device=dev)  # zero before first use (counters)
 
         def fused():
             sp = torch.cuda.current_stream().cuda_stream
