@@ -144,6 +144,27 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
                  void* y, int32_t out_dtype, int64_t N, int64_t K,
                  void* workspace, size_t workspace_bytes, void* hip_stream);
 
+/* Tuning form of nf4_gemm_ref.  kernel: 0 = library choice,
+ * NF4DQ_GEMM_STREAM (K % 256 == 0; waves 4/8/16, depth = chunks in flight per
+ * wave 2/4 (16 waves only when M <= 16), strips = 16-column strips per workgroup
+ * 1/2/4 dividing waves) or NF4DQ_GEMM_K128 (waves 4/8, depth 1/2/4 (<= 2 when
+ * M > 16), strips ignored).  ksplit: K slices reduced across workgroups.
+ * An invalid combination returns NF4DQ_ERR_ARG. */
+#define NF4DQ_GEMM_K128 1
+#define NF4DQ_GEMM_STREAM 2
+typedef struct nf4_gemm_cfg {
+    int32_t kernel;
+    int32_t waves;
+    int32_t depth;
+    int32_t ksplit;
+    int32_t strips;
+} nf4_gemm_cfg;
+size_t nf4_gemm_workspace_bytes_cfg(int64_t M, int64_t N, int64_t K, const nf4_gemm_cfg* cfg);
+int nf4_gemm_ref_cfg(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len,
+                     const uint8_t* absmax_q, int64_t nb, const float* absmax2, int64_t n2,
+                     void* y, int32_t out_dtype, int64_t N, int64_t K,
+                     void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfg, void* hip_stream);
+
 /* Human-readable text for a return code (static storage). */
 const char* nf4_strerror(int code);
 

@@ -59,6 +59,15 @@ class LaunchCfg(ctypes.Structure):
 
 
 CFG_NT_LOADS = 1
+GEMM_K128 = 1
+GEMM_STREAM = 2
+
+
+class GemmCfg(ctypes.Structure):
+    """nf4_gemm_cfg (include/nf4_dequant.h)."""
+
+    _fields_ = [("kernel", ctypes.c_int32), ("waves", ctypes.c_int32), ("depth", ctypes.c_int32),
+                ("ksplit", ctypes.c_int32), ("strips", ctypes.c_int32)]
 
 
 # name -> (restype, argtypes); every symbol include/nf4_dequant.h declares.
@@ -74,6 +83,9 @@ SIGNATURES = {
     "nf4_gemm_workspace_bytes": (ctypes.c_size_t, [_I64, _I64, _I64]),
     "nf4_gemm_ref": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I32, _I64, _I64, _P, ctypes.c_size_t,
                                     _P]),
+    "nf4_gemm_workspace_bytes_cfg": (ctypes.c_size_t, [_I64, _I64, _I64, ctypes.POINTER(GemmCfg)]),
+    "nf4_gemm_ref_cfg": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I32, _I64, _I64, _P,
+                                        ctypes.c_size_t, ctypes.POINTER(GemmCfg), _P]),
     "nf4_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "nf4_version": (ctypes.c_char_p, []),
 }

@@ -35,7 +35,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kGemmWaves = 8;
 constexpr int kAuxSc1 = 16;  // write-through stores / L2-bypassing loads (cross-XCD hand-off)
 
 template <int DT>
@@ -124,13 +123,14 @@ __device__ __forceinline__ void chunk_mma(const Chunk<MT>& in, const float* lut,
     }
 }
 
-// Workgroup = kGemmWaves waves owning 16 output columns of one K slice; wave
-// w takes every kGemmWaves-th group of D chunks, D chunks in flight at a time;
-// the waves' partial sums are combined through LDS (fixed order).
-template <int DT, int MT, int D>
-__global__ __launch_bounds__(64 * kGemmWaves) void nf4_gemm_smallm_kernel(const GemmArgs A) {
+// Workgroup = WV waves owning 16 output columns of one K slice; wave w takes
+// every WV-th group of D chunks, D chunks in flight at a time; the waves'
+// partial sums are combined through LDS (fixed order).
+template <int DT, int MT, int D, int WV>
+__global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs A) {
+    constexpr int kGemmWaves = WV;
     __shared__ __attribute__((aligned(16))) float lut[20];  // 16 codes + the last-arriver flag
-    __shared__ __attribute__((aligned(16))) f32x4 red[kGemmWaves][MT][64];
+    __shared__ __attribute__((aligned(16))) f32x4 red[WV][MT][64];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t nl = lane & 15u, kh = lane >> 4;
@@ -223,24 +223,399 @@ __global__ __launch_bounds__(64 * kGemmWaves) void nf4_gemm_smallm_kernel(const 
     }
 }
 
-// K split across workgroups only when there are too few 16-column strips to
-// give every CU two workgroups; each slice keeps >= kGemmWaves chunks.
-uint32_t choose_ksplit(int64_t M, int64_t N, int64_t K) {
-    (void)M;
-    const int64_t strips = N / 16, chunks = K / kChunkK;
-    int64_t ks = (512 + strips - 1) / strips;
-    const int64_t max_ks = chunks / kGemmWaves > 0 ? chunks / kGemmWaves : 1;
-    if (ks > max_ks) ks = max_ks;
-    return (uint32_t)(ks < 1 ? 1 : ks);
+// ---------------------------------------------------------------------------
+// Streaming decode kernel (K % 256 == 0).  Weight bytes are the only operand
+// that comes from HBM, so a wave keeps P chunks of them in flight in registers
+// (a ring refilled right after each chunk is consumed: counted vmcnt, never a
+// drain) and takes everything else from LDS: the activation slice x[0:M, k0:k1]
+// is staged once per workgroup, the 16 NF4 codes and the 256 values q/127 are
+// tables there.  A chunk is 256 deep: one 128-byte line of each of the strip's
+// 16 weight rows; lane (nl, kh) holds 32 bytes = exactly one 64-block (one
+// scale) of row nl, i.e. eight MFMA B fragments.  Waves of a workgroup split
+// the strip's K slice (interleaved chunks, so neighbouring waves read
+// neighbouring lines) and T strips; partial sums meet in LDS in a fixed order.
+constexpr uint32_t kSChunkK = 256;
+
+constexpr int kXR = 8;               // x staging: 16-byte pieces per thread and row tile
+constexpr uint32_t kLdsX = 0;        // dynamic LDS: [x slice][zero block][partials]
+
+struct StreamArgs {
+    const uint8_t* packed;
+    const uint8_t* a1;
+    const float* a2;
+    const void* x;
+    void* y;
+    float* slab;
+    uint32_t* counters;
+    uint32_t M, N, K;
+    uint32_t strip_groups;  // N / (16 T)
+    uint32_t T, parts;      // strips per workgroup, K parts per strip
+    uint32_t ksplit, cps;   // K slices, chunks per slice
+    uint32_t cpp;           // chunks per K part (a part's chunks are contiguous)
+    uint32_t chunks;        // K / 256
+    uint32_t bpr, groups;   // K / 64, ceil(bpr / 4)
+    uint32_t nb_bytes, n2_bytes;
+    FastDiv nb, n2;
+    FastDiv ppr;            // 16-byte x pieces per staged row (cps * 32)
+    uint32_t xstride;       // LDS bytes per staged x row
+    uint32_t zero_off;      // 128 zero bytes: the A operand of rows >= M
+    uint32_t red_off;       // [W][MT][64] f32x4 partial sums
+    unsigned long long* stamps;  // NF4_STREAM_DEBUG == 3 only
+};
+
+#if NF4_STREAM_DEBUG == 3
+#define NF4_STAMP(slot_)                                                                              \
+    do {                                                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        unsigned long long t_;                                                                        \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+        if (lane == 0) A.stamps[(blockIdx.x * W + wave) * 8u + (slot_)] = t_;                         \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+    } while (0)
+#else
+#define NF4_STAMP(slot_) \
+    do {                 \
+    } while (0)
+#endif
+
+struct SSlot {
+    u32x4 w0, w1;
+    uint32_t qa;
+    float qb;
+};
+
+// Diagnostic builds only (tools/Makefile): 1 = loads without the dequant/MMA
+// body, 2 = the body on register-made data without weight loads, 3 = per-wave
+// s_memrealtime stamps (start, prologue done, loop done, end) into the
+// workspace after the counter region (ksplit 1 only).
+#ifndef NF4_STREAM_DEBUG
+#define NF4_STREAM_DEBUG 0
+#endif
+
+constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads return 0, no traffic
+
+template <bool VS, class Args>
+__device__ __forceinline__ void sslot_issue(const Args& A, __amdgpu_buffer_rsrc_t rw,
+                                            __amdgpu_buffer_rsrc_t ra1, __amdgpu_buffer_rsrc_t ra2, uint32_t c,
+                                            bool valid, uint32_t row, uint32_t kh, SSlot& s) {
+    // `valid` is wave-uniform; past the wave's last chunk the offsets get bit 31
+    // (beyond every range: zeros, no traffic) -- arithmetic, not a branch, so
+    // the waitcnt pass sees one straight-line ring
+    const uint32_t oob = valid ? 0u : kOob;
+    const uint32_t woff = (row * (A.K >> 1) + c * 128u + kh * 32u) | oob;
+#if NF4_STREAM_DEBUG == 2 || NF4_STREAM_DEBUG == 5
+    s.w0 = u32x4{woff, woff * 3u, woff ^ 0x5555u, c};
+    s.w1 = u32x4{c * 7u, woff + c, row, kh};
+    s.qa = (woff >> 3) & 0xFFu;
+    s.qb = 0.001f;
+    (void)rw; (void)ra1; (void)ra2;
+    return;
+#endif
+    s.w0 = __builtin_amdgcn_raw_buffer_load_b128(rw, woff, 0, 0);
+    s.w1 = __builtin_amdgcn_raw_buffer_load_b128(rw, woff + 16u, 0, 0);
+    if constexpr (!VS) {
+        // block 4c + kh of the row; its nested group is c (reference wraps, :173-186)
+        const uint32_t i1 = fmodu(row * A.bpr + 4u * c + kh, A.nb) | oob;
+        const uint32_t i2 = (fmodu(row * A.groups + c, A.n2) * 4u) | oob;
+#if NF4_STREAM_DEBUG == 4
+        s.qa = i1 & 0xFFu;
+        s.qb = __uint_as_float(i2 & 0x3FFFFFFFu);
+        (void)ra1;
+        (void)ra2;
+#else
+        s.qa = __builtin_amdgcn_raw_buffer_load_b8(ra1, i1, 0, 0);
+        s.qb = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra2, i2, 0, 0));
+#endif
+    }
+}
+
+// The dequant body: codes are looked up in pairs from a 256-entry table
+// (code[b >> 4], code[b & 15]) per packed byte b, replicated into 32 lane slots
+// so that lane l reads bank pair 2 (l mod 32): one conflict-free ds_read_b64
+// per two weights, its LDS address one v_perm_b32 (byte b into bits 8..15, the
+// lane's slot offset into bits 0..7).  Then the fp32 products with the block
+// scale and one RNE pack per pair: 1.5 VALU per weight.
+template <int DT, int MT>
+__device__ __forceinline__ void sslot_mma(const SSlot& s, uint32_t qa, float qb, const f32x2* ptab,
+                                          const float* qtab, const char* smem, uint32_t slot8,
+                                          const uint32_t (&xa)[MT], f32x4 (&acc)[MT]) {
+    const float sc = qtab[qa] * qb;  // (:45, :97-98)
+    const f32x2 sc2 = {sc, sc};
+    const char* pt = reinterpret_cast<const char*>(ptab);
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+        const uint32_t wd = st < 4 ? s.w0[st] : s.w1[st - 4];
+        uint32_t bw[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t addr = __builtin_amdgcn_perm(wd, slot8, 0x0C0C0000u | ((4u + b) << 8));
+            const f32x2 v = *reinterpret_cast<const f32x2*>(pt + addr) * sc2;  // fp32 products (:97-98)
+            bw[b] = pack2<DT>(v.x, v.y);                                         // RNE (:109-110)
+        }
+        const u32x4 bq = {bw[0], bw[1], bw[2], bw[3]};
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const u32x4 a = *reinterpret_cast<const u32x4*>(smem + xa[mt] + 16u * st);
+            if constexpr (DT == NF4DQ_BF16) {
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                                  __builtin_bit_cast(bf16x8, bq), acc[mt], 0, 0, 0);
+            } else {
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                                 __builtin_bit_cast(f16x8, bq), acc[mt], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// VS: vector scales -- no absmax wrap (nb >= N K / 64, n2 >= N groups) and a
+// wave's chunks all in its ring (cpp <= P): its 4 x 4 absmax bytes and 4
+// nested scales come in two 16-byte loads up front instead of two gathers per chunk.
+template <int DT, int MT, int W, int P, bool VS>
+__global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ __attribute__((aligned(16))) f32x2 ptab[256 * 32];  // 64 KiB pair table, built per workgroup
+    __shared__ __attribute__((aligned(16))) float lut[16];
+    __shared__ float qtab[256];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar control flow below
+    const uint32_t nl = lane & 15u, kh = lane >> 4;
+    const uint32_t sg = blockIdx.x % A.strip_groups, ks = blockIdx.x / A.strip_groups;
+    const uint32_t strip = sg * A.T + wave % A.T, part = wave / A.T;
+    const uint32_t row = strip * 16u + nl;
+    const uint32_t s0 = ks * A.cps;
+    const uint32_t s1 = s0 + A.cps < A.chunks ? s0 + A.cps : A.chunks;
+    const uint32_t nloc = s1 - s0;
+    const uint32_t l0 = part * A.cpp;  // first chunk of this wave within the slice
+    const uint32_t cnt = nloc > l0 ? (nloc - l0 < A.cpp ? nloc - l0 : A.cpp) : 0u;
+    NF4_STAMP(0);
+#if NF4_STREAM_DEBUG == 3
+    if (lane == 0) {
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        A.stamps[(blockIdx.x * W + wave) * 8u + 6u] = hw;
+        A.stamps[(blockIdx.x * W + wave) * 8u + 7u] = xcc;
+    }
+#endif
+
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.N * (A.K >> 1), kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)A.a1, 0, A.nb_bytes, kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)A.a2, 0, A.n2_bytes, kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
+
+    // 1. activation slice loads first (the counted waits below then leave the weight ring in flight)
+    const uint32_t pieces = A.M * A.ppr.d;
+    constexpr int XR = kXR * MT;
+    u32x4 xv[XR];
+    uint32_t xdst[XR];
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+        const uint32_t p = tid + (uint32_t)i * 64u * W;
+        const uint32_t r = fdiv(p, A.ppr), q = p - r * A.ppr.d;
+        const bool ok = p < pieces && s0 * 256u + q * 8u < A.K;
+        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? (r * A.K + s0 * 256u) * 2u + q * 16u : kOob, 0, 0);
+        xdst[i] = p < pieces ? kLdsX + r * A.xstride + q * 16u : 0xFFFFFFFFu;
+    }
+    // 2. the weight ring (VS: the wave's scales first)
+    // (issue order = the loop's: slot by slot, w0 w1 qa qb -- the scheduler must
+    // not regroup them, or the waitcnt pass merges two orders into a drain)
+    u32x4 a1v = {0u, 0u, 0u, 0u};
+    u32x4 a2v = {0u, 0u, 0u, 0u};
+    if constexpr (VS) {
+        const uint32_t cf = s0 + l0;
+        const uint32_t oob = cnt ? 0u : kOob;
+        a1v = __builtin_amdgcn_raw_buffer_load_b128(ra1, (row * A.bpr + 4u * cf) | oob, 0, 0);
+        a2v = __builtin_amdgcn_raw_buffer_load_b128(ra2, ((row * A.groups + cf) * 4u) | oob, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    SSlot ring[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        sslot_issue<VS>(A, rw, ra1, ra2, s0 + l0 + (uint32_t)j, (uint32_t)j < cnt, row, kh, ring[j]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // 3. tables, then the staged slice (waits for the x loads only)
+    write_lut(lut);
+    if (tid < 256u) qtab[tid] = (float)tid / 127.0f;  // IEEE division
+    if (tid < 8u) *reinterpret_cast<u32x4*>(smem + A.zero_off + 16u * tid) = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < XR; ++i)
+        if (xdst[i] != 0xFFFFFFFFu) *reinterpret_cast<u32x4*>(smem + xdst[i]) = xv[i];
+    __syncthreads();
+    // the pair table: entry e of lane slot t at byte 256 e + 8 t
+    for (uint32_t i = tid; i < 256u * 32u; i += 64u * W) {
+        const uint32_t e = i >> 5;
+        ptab[i] = f32x2{lut[e >> 4], lut[e & 15u]};
+    }
+    __syncthreads();
+    NF4_STAMP(1);
+#if NF4_STREAM_DEBUG == 3
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#endif
+
+    uint32_t xa0[MT];
+    bool live[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        live[mt] = 16u * mt + nl < A.M;
+        xa0[mt] = live[mt] ? kLdsX + (16u * mt + nl) * A.xstride + kh * 128u : A.zero_off;
+    }
+    const uint32_t slot8 = (lane & 31u) * 8u;
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (uint32_t base = 0; base < cnt; base += P) {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const uint32_t jj = base + (uint32_t)j;
+            if (jj < cnt) {
+                const uint32_t l = l0 + jj;  // chunk within the slice
+                uint32_t xa[MT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) xa[mt] = live[mt] ? xa0[mt] + l * 512u : xa0[mt];
+                // VS: cnt <= P, so jj == j here and the vector lanes are static
+                const uint32_t qa = VS ? (a1v[j] >> (8u * kh)) & 0xFFu : ring[j].qa;
+                const float qb = VS ? __uint_as_float(a2v[j]) : ring[j].qb;
+#if NF4_STREAM_DEBUG == 1 || NF4_STREAM_DEBUG == 4 || NF4_STREAM_DEBUG == 5
+                acc[0][0] += __uint_as_float((ring[j].w0[0] ^ ring[j].w1[3] ^ qa) & 0x3FFFFFFFu) * qb;
+                (void)xa;
+#else
+                sslot_mma<DT, MT>(ring[j], qa, qb, ptab, qtab, smem, slot8, xa, acc);
+#endif
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (VS) continue;  // the whole range is in the ring already
+            const uint32_t jn = jj + P;
+            sslot_issue<VS>(A, rw, ra1, ra2, s0 + l0 + jn, jn < cnt, row, kh, ring[j]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    NF4_STAMP(2);
+    // 4. the strip's K parts meet in LDS, in part order (the partials reuse the
+    // x slice's LDS once every wave is done reading it)
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smem + A.red_off);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) red[(wave * MT + mt) * 64u + lane] = acc[mt];
+    __syncthreads();
+    if (part != 0) return;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        f32x4 s = red[(wave * MT + mt) * 64u + lane];
+        for (uint32_t p = 1; p < A.parts; ++p) s += red[((wave + p * A.T) * MT + mt) * 64u + lane];
+        acc[mt] = s;
+    }
+    // acc[mt][r] = Y[16 mt + 4 kh + r][row]
+    if (A.ksplit == 1) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t m = 16u * mt + 4u * kh + r;
+                if (m < A.M) store_y<DT>(A.y, m * A.N + row, acc[mt][r]);
+            }
+        NF4_STAMP(3);
+        return;
+    }
+    // 5. split-K across workgroups: the hand-off of nf4_gemm_smallm_kernel, per strip
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)A.slab, 0, A.ksplit * A.M * A.N * 4u, kRsrcFlags);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t m = 16u * mt + 4u * kh + r;
+            const uint32_t off = m < A.M ? ((ks * A.M + m) * A.N + row) * 4u : kOob;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][r]), rs, off, 0, kAuxSc1);
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t last = 0;
+    if (lane == 0) {
+        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[strip], 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        last = ticket == A.ksplit - 1u;
+        if (last) __hip_atomic_store(&A.counters[strip], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last = __builtin_amdgcn_readfirstlane(last);
+    if (!last) return;
+    for (uint32_t i = lane; i < A.M * 16u; i += 64u) {
+        const uint32_t m = i >> 4;
+        const uint32_t n = strip * 16u + (i & 15u);
+        float sum = 0.0f;
+        for (uint32_t k = 0; k < A.ksplit; ++k)
+            sum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ((k * A.M + m) * A.N + n) * 4u, 0, kAuxSc1));
+        store_y<DT>(A.y, m * A.N + n, sum);
+    }
+}
+
+
+// ---- decomposition choice --------------------------------------------------
+constexpr uint32_t kLdsPerCu = 160 * 1024;
+constexpr uint32_t kStreamStatic = 256 * 32 * 8 + 64 + 1024;  // pair table, code LUT, q/127 table
+constexpr uint32_t kStreamLdsCap = kLdsPerCu - kStreamStatic;  // dynamic part
+
+struct StreamPlan {
+    uint32_t cps, xstride, zero_off, red_off, lds;
+};
+
+static StreamPlan stream_plan(int64_t M, int64_t K, const nf4_gemm_cfg& c) {
+    const uint32_t chunks = (uint32_t)(K / kSChunkK);
+    const uint32_t mt = (uint32_t)((M + 15) / 16);
+    StreamPlan p{};
+    p.cps = (chunks + (uint32_t)c.ksplit - 1) / (uint32_t)c.ksplit;
+    p.xstride = p.cps * 512u + 16u;  // +16 B: consecutive rows start 4 banks apart
+    p.zero_off = kLdsX + (uint32_t)M * p.xstride;
+    p.red_off = kLdsX;
+    const uint32_t xend = p.zero_off + 128u, rend = p.red_off + (uint32_t)c.waves * mt * 1024u;
+    p.lds = xend > rend ? xend : rend;
+    return p;
+}
+
+static bool stream_fits(int64_t M, int64_t K, const nf4_gemm_cfg& c) {
+    const StreamPlan p = stream_plan(M, K, c);
+    const int64_t xr = kXR * ((M + 15) / 16);
+    return p.lds <= kStreamLdsCap && M * (int64_t)p.cps * 32 <= xr * 64 * c.waves;
+}
+
+// Defaults, from tools/sweep_gemm.py on MI355X (Llama-3-8B shapes, M = 1, 4, 16, 32):
+// the streaming kernel for decode-sized M (8 waves, 2 chunks in flight, whole K
+// per workgroup; 4 strips per workgroup for wide N; a 2-way K split for long K
+// once M > 1), the 128-deep kernel for 16 < M and for narrow N at M = 16.
+nf4_gemm_cfg default_gemm_cfg(int64_t M, int64_t N, int64_t K) {
+    if (K % kSChunkK == 0 && (M <= 8 || (M <= 16 && N >= 8192))) {
+        nf4_gemm_cfg c{NF4DQ_GEMM_STREAM, 8, 2, 1, N >= 8192 ? 4 : 1};
+        if (M > 8) c.ksplit = 2;
+        else if (M > 1 && K >= 8192) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 2, 2};
+        while (c.ksplit < K / kSChunkK && !stream_fits(M, K, c)) ++c.ksplit;
+        if (N % (16 * c.strips)) c.strips = 1;
+        return c;
+    }
+    nf4_gemm_cfg c{NF4DQ_GEMM_K128, 8, M > 16 ? 1 : 2, 1, 1};
+    return c;
+}
+
+bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
+    if (c.kernel == NF4DQ_GEMM_STREAM) {
+        if (K % kSChunkK) return false;
+        if (c.waves != 4 && c.waves != 8 && c.waves != 16) return false;
+        if (c.depth != 2 && c.depth != 4) return false;
+        if (c.waves == 16 && M > 16) return false;
+        if (c.strips != 1 && c.strips != 2 && c.strips != 4) return false;
+        if (c.waves % c.strips || N % (16 * c.strips)) return false;
+        if (c.ksplit < 1 || c.ksplit > K / kSChunkK) return false;
+        return stream_fits(M, K, c);
+    }
+    if (c.kernel != NF4DQ_GEMM_K128) return false;
+    if (c.waves != 4 && c.waves != 8) return false;
+    if (M > 16 ? (c.depth != 1 && c.depth != 2) : (c.depth != 1 && c.depth != 2 && c.depth != 4)) return false;
+    return c.ksplit >= 1 && c.ksplit <= K / kChunkK && c.ksplit <= 64;
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 inline int hip_rc2(hipError_t e) { return e == hipSuccess ? NF4DQ_OK : NF4DQ_ERR_HIP_BASE + (int)e; }
-
-}  // namespace
-
-extern "C" {
 
 // Workspace: [64 KiB of uint32 ticket counters][ksplit * M * N fp32 partials].
 // The counter region has a fixed size so that no call's partials ever overlay
@@ -248,16 +623,14 @@ extern "C" {
 constexpr size_t kCounterBytes = 64 * 1024;
 static size_t counters_bytes(int64_t) { return kCounterBytes; }
 
-size_t nf4_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+static size_t workspace_for(int64_t M, int64_t N, int64_t K, const nf4_gemm_cfg& c) {
     if (M <= 0 || N <= 0 || K <= 0 || N % 64 || K % kChunkK) return 0;
-    const uint32_t ks = choose_ksplit(M, N, K);
-    return ks > 1 ? counters_bytes(N) + (size_t)ks * (size_t)M * (size_t)N * sizeof(float) : 0;
+    return c.ksplit > 1 ? counters_bytes(N) + (size_t)c.ksplit * (size_t)M * (size_t)N * sizeof(float) : 0;
 }
 
-int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,
-                 int64_t nb, const float* absmax2, int64_t n2, void* y, int32_t dtype, int64_t N, int64_t K,
-                 void* workspace, size_t workspace_bytes, void* hip_stream) {
-    hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,
+                     int64_t nb, const float* absmax2, int64_t n2, void* y, int32_t dtype, int64_t N, int64_t K,
+                     void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfgp, hipStream_t st) {
     if (dtype != NF4DQ_F16 && dtype != NF4DQ_BF16) return NF4DQ_ERR_ARG;
     if (M < 0 || N < 0 || K < 0 || nb <= 0 || n2 <= 0) return NF4DQ_ERR_ARG;
     if (M == 0 || N == 0) return NF4DQ_OK;
@@ -265,9 +638,93 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
     if (M > NF4DQ_GEMM_MAX_M || N % 64 || K % kChunkK || packed_len != N * (K / 2)) return NF4DQ_ERR_SHAPE;
     if ((size_t)(N / 16) * 4 > kCounterBytes) return NF4DQ_ERR_TOO_LARGE;
     if (packed_len >= (int64_t(1) << 31) || M * K * 2 >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
-    const uint32_t ks = choose_ksplit(M, N, K);
-    const size_t need = nf4_gemm_workspace_bytes(M, N, K);
+    nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, N, K);
+    if (cfg.kernel == 0) {
+        const nf4_gemm_cfg d = default_gemm_cfg(M, N, K);
+        cfg.kernel = d.kernel;
+    }
+    if (!valid_gemm_cfg(cfg, M, N, K)) return NF4DQ_ERR_ARG;
+    const uint32_t ks = (uint32_t)cfg.ksplit;
+    const size_t need = workspace_for(M, N, K, cfg);
     if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
+    if (cfg.kernel == NF4DQ_GEMM_STREAM) {
+        const StreamPlan pl = stream_plan(M, K, cfg);
+        StreamArgs S{};
+        S.packed = packed;
+        S.a1 = absmax_q;
+        S.a2 = absmax2;
+        S.x = x;
+        S.y = y;
+        S.counters = reinterpret_cast<uint32_t*>(workspace);
+        S.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + counters_bytes(N)) : nullptr;
+        S.M = (uint32_t)M;
+        S.N = (uint32_t)N;
+        S.K = (uint32_t)K;
+        S.T = (uint32_t)cfg.strips;
+        S.parts = (uint32_t)(cfg.waves / cfg.strips);
+        S.strip_groups = (uint32_t)(N / (16 * cfg.strips));
+        S.ksplit = ks;
+        S.chunks = (uint32_t)(K / kSChunkK);
+        S.cps = pl.cps;
+        S.bpr = (uint32_t)(K / 64);
+        S.groups = (S.bpr + 3) / 4;
+        const int64_t nbc = nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : nb;
+        const int64_t n2c = n2 > (int64_t(1) << 29) ? (int64_t(1) << 29) : n2;
+        S.nb = make_fastdiv((uint32_t)nbc);
+        S.n2 = make_fastdiv((uint32_t)n2c);
+        S.nb_bytes = (uint32_t)nbc;
+        S.n2_bytes = (uint32_t)(n2c * 4);
+        S.ppr = make_fastdiv(pl.cps * 32u);
+        S.xstride = pl.xstride;
+        S.zero_off = pl.zero_off;
+        S.red_off = pl.red_off;
+#if NF4_STREAM_DEBUG == 3
+        S.stamps = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + kCounterBytes);
+#endif
+        S.cpp = (pl.cps + S.parts - 1) / S.parts;
+        // vector scales: no absmax wrap anywhere in the matrix, and each wave's chunks fit its ring
+        const bool vs = nb >= N * (K / 64) && n2 >= N * (int64_t)S.groups && S.cpp <= (uint32_t)cfg.depth;
+        const dim3 grid(S.strip_groups * ks), block(64 * cfg.waves);
+        const int mt = (int)((M + 15) / 16);
+#define NF4_K1(DT_, MT_, W_, P_, VS_)                                                                       \
+    do {                                                                                                    \
+        static bool attr_ = false; /* static + dynamic LDS above 64 KiB needs the opt-in */                  \
+        if (!attr_) {                                                                                       \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_stream_kernel<DT_, MT_, W_, P_, VS_>), \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsCap);      \
+            attr_ = true;                                                                                   \
+        }                                                                                                   \
+        hipLaunchKernelGGL((nf4_gemm_stream_kernel<DT_, MT_, W_, P_, VS_>), grid, block, pl.lds, st, S);    \
+    } while (0)
+#define NF4_K(DT_, MT_, W_, P_)                 \
+    do {                                        \
+        if (vs) NF4_K1(DT_, MT_, W_, P_, true); \
+        else NF4_K1(DT_, MT_, W_, P_, false);   \
+    } while (0)
+#define NF4_P(DT_, MT_, W_)                                \
+    do {                                                   \
+        if (cfg.depth == 2) NF4_K(DT_, MT_, W_, 2);        \
+        else NF4_K(DT_, MT_, W_, 4);                       \
+    } while (0)
+#define NF4_WW(DT_)                                        \
+    do {                                                   \
+        if (mt == 1) {                                     \
+            if (cfg.waves == 4) NF4_P(DT_, 1, 4);          \
+            else if (cfg.waves == 8) NF4_P(DT_, 1, 8);     \
+            else NF4_P(DT_, 1, 16);                        \
+        } else { /* 16 waves only for M <= 16 */           \
+            if (cfg.waves == 4) NF4_P(DT_, 2, 4);          \
+            else NF4_P(DT_, 2, 8);                         \
+        }                                                  \
+    } while (0)
+        if (dtype == NF4DQ_BF16) NF4_WW(NF4DQ_BF16);
+        else NF4_WW(NF4DQ_F16);
+#undef NF4_WW
+#undef NF4_P
+#undef NF4_K
+#undef NF4_K1
+        return hip_rc2(hipGetLastError());
+    }
     GemmArgs A{};
     A.packed = packed;
     A.a1 = absmax_q;
@@ -287,19 +744,59 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
     A.groups = (A.bpr + 3) / 4;
     A.nb = make_fastdiv((uint32_t)(nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : nb));
     A.n2 = make_fastdiv((uint32_t)(n2 > (int64_t(1) << 31) ? (int64_t(1) << 31) : n2));
-    const dim3 grid(A.col_groups * ks), block(64 * kGemmWaves);
+    const dim3 grid(A.col_groups * ks), block(64 * cfg.waves);
     const int mt = (int)((M + 15) / 16);
-#define NF4_G(DT_, MT_, D_) hipLaunchKernelGGL((nf4_gemm_smallm_kernel<DT_, MT_, D_>), grid, block, 0, st, A)
-#define NF4_S(DT_)                          \
-    do {                                    \
-        if (mt == 1) NF4_G(DT_, 1, 4);      \
-        else NF4_G(DT_, 2, 2);              \
+#define NF4_G(DT_, MT_, D_, W_) hipLaunchKernelGGL((nf4_gemm_smallm_kernel<DT_, MT_, D_, W_>), grid, block, 0, st, A)
+#define NF4_W(DT_, MT_, D_)                        \
+    do {                                           \
+        if (cfg.waves == 8) NF4_G(DT_, MT_, D_, 8); \
+        else NF4_G(DT_, MT_, D_, 4);               \
+    } while (0)
+#define NF4_S(DT_)                                  \
+    do {                                            \
+        if (mt == 1) {                              \
+            if (cfg.depth == 4) NF4_W(DT_, 1, 4);   \
+            else if (cfg.depth == 2) NF4_W(DT_, 1, 2); \
+            else NF4_W(DT_, 1, 1);                  \
+        } else {                                    \
+            if (cfg.depth == 2) NF4_W(DT_, 2, 2);   \
+            else NF4_W(DT_, 2, 1);                  \
+        }                                           \
     } while (0)
     if (dtype == NF4DQ_BF16) NF4_S(NF4DQ_BF16);
     else NF4_S(NF4DQ_F16);
 #undef NF4_S
+#undef NF4_W
 #undef NF4_G
     return hip_rc2(hipGetLastError());
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t nf4_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+    if (M <= 0 || N <= 0 || K <= 0 || N % 64 || K % kChunkK) return 0;
+    return workspace_for(M, N, K, default_gemm_cfg(M, N, K));
+}
+
+size_t nf4_gemm_workspace_bytes_cfg(int64_t M, int64_t N, int64_t K, const nf4_gemm_cfg* cfg) {
+    if (!cfg) return nf4_gemm_workspace_bytes(M, N, K);
+    return workspace_for(M, N, K, *cfg);
+}
+
+int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,
+                 int64_t nb, const float* absmax2, int64_t n2, void* y, int32_t dtype, int64_t N, int64_t K,
+                 void* workspace, size_t workspace_bytes, void* hip_stream) {
+    return gemm_impl(x, M, packed, packed_len, absmax_q, nb, absmax2, n2, y, dtype, N, K, workspace, workspace_bytes,
+                     nullptr, reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+int nf4_gemm_ref_cfg(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,
+                     int64_t nb, const float* absmax2, int64_t n2, void* y, int32_t dtype, int64_t N, int64_t K,
+                     void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfg, void* hip_stream) {
+    return gemm_impl(x, M, packed, packed_len, absmax_q, nb, absmax2, n2, y, dtype, N, K, workspace, workspace_bytes,
+                     cfg, reinterpret_cast<hipStream_t>(hip_stream));
 }
 
 }  // extern "C"

@@ -108,9 +108,14 @@ def test_abi_rejects_non_fast_shapes(gpu):
     assert L.nf4_gemm_ref(F, 1, F, 32 * 64, F, 64, F, 1, F, _lib.BF16, 32, 128, None, 0, None) == _lib.ERR_SHAPE
     assert L.nf4_gemm_ref(F, 1, F, 64 * 48, F, 64, F, 1, F, _lib.BF16, 64, 96, None, 0, None) == _lib.ERR_SHAPE
     assert L.nf4_gemm_ref(F, 1, F, 64 * 64, F, 64, F, 1, F, _lib.F32, 64, 128, None, 0, None) == _lib.ERR_ARG
-    need = L.nf4_gemm_workspace_bytes(1, 4096, 4096)
+    import ctypes
+
+    c = _lib.GemmCfg(_lib.GEMM_STREAM, 8, 4, 2, 1)
+    need = L.nf4_gemm_workspace_bytes_cfg(1, 4096, 4096, ctypes.byref(c))
     assert need > 0
-    assert L.nf4_gemm_ref(F, 1, F, 4096 * 2048, F, 64, F, 1, F, _lib.BF16, 4096, 4096, None, 0, None) == _lib.ERR_ARG
+    # a K split without its workspace is an argument error, not a fault
+    assert L.nf4_gemm_ref_cfg(F, 1, F, 4096 * 2048, F, 64, F, 1, F, _lib.BF16, 4096, 4096, None, 0,
+                              ctypes.byref(c), None) == _lib.ERR_ARG
 
 
 def test_workspace_reuse_across_shapes(coracle, gpu):
@@ -123,3 +128,74 @@ def test_workspace_reuse_across_shapes(coracle, gpu):
         mod = make_module(packed, a1, a2, N, K, "bf16", gpu)
         xt, xb = _x_bits(M, K, "bf16", seed=M + 1)
         _check(nf4_linear(xt.to(gpu), mod), xb, W, "bf16")
+
+
+def _gemm_cfg_call(L, _lib, xt, mod_t, y, dt_code, N, K, cfg):
+    import ctypes
+
+    packed, a1, a2 = mod_t
+    M = xt.shape[0]
+    wsz = L.nf4_gemm_workspace_bytes_cfg(M, N, K, ctypes.byref(cfg))
+    ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=xt.device)
+    rc = L.nf4_gemm_ref_cfg(xt.data_ptr(), M, packed.data_ptr(), packed.numel(), a1.data_ptr(), a1.numel(),
+                            a2.data_ptr(), a2.numel(), y.data_ptr(), dt_code, N, K, ws.data_ptr(), wsz,
+                            ctypes.byref(cfg), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return rc
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 4096), (5, 128, 2816), (16, 64, 1536), (32, 128, 2048),
+                                   (1, 8192, 512), (3, 4160, 1280)])
+def test_every_decomposition_agrees_with_oracle(coracle, gpu, dt, M, N, K):
+    """Each kernel / waves / depth / strips / K-split combination the tuning ABI accepts."""
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    packed, a1, a2 = O.make_inputs(N, K, seed=N * 3 + K + M, a2_kind="normal")
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16)
+    t = (torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu))
+    xt, xb = _x_bits(M, K, dt, seed=M * 5 + 1)
+    x = xt.to(gpu)
+    code = _lib.BF16 if dt == "bf16" else _lib.F16
+    # the float64 oracle and its tolerance once; each config is compared on the GPU
+    xf, wf = _bits_to_f64(xb, dt), _bits_to_f64(W, dt)
+    ref = torch.from_numpy(xf @ wf.T).to(gpu)
+    p = 8 if dt == "bf16" else 10
+    tol = torch.from_numpy(2.0 ** -p * np.abs(xf @ wf.T) + 2.0 ** -20 * (np.abs(xf) @ np.abs(wf).T)).to(gpu)
+    y = torch.empty((M, N), dtype=x.dtype, device=gpu)
+    ran = 0
+    for kernel in (_lib.GEMM_STREAM, _lib.GEMM_K128):
+        for waves in (4, 8, 16):
+            for depth in (1, 2, 4, 8):
+                for strips in ((1, 2, 4) if kernel != _lib.GEMM_K128 else (1,)):
+                    for ks in (1, 3):
+                        cfg = _lib.GemmCfg(kernel, waves, depth, ks, strips)
+                        y.fill_(float("nan"))
+                        rc = _gemm_cfg_call(L, _lib, x, t, y, code, N, K, cfg)
+                        if rc == _lib.ERR_ARG:
+                            continue
+                        assert rc == 0, (kernel, waves, depth, strips, ks, rc)
+                        bad = ((y.double() - ref).abs() > tol) | torch.isnan(y)
+                        assert not bool(bad.any()), (kernel, waves, depth, strips, ks, int(bad.sum()))
+                        ran += 1
+    assert ran >= 12
+
+
+def test_invalid_decompositions_rejected(gpu):
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    import ctypes
+
+    F = 0x1000
+    for cfg in [(_lib.GEMM_STREAM, 6, 4, 1, 1), (_lib.GEMM_STREAM, 8, 3, 1, 1), (_lib.GEMM_STREAM, 8, 4, 1, 3),
+                (_lib.GEMM_STREAM, 4, 4, 1, 8), (_lib.GEMM_STREAM, 8, 4, 0, 1), (_lib.GEMM_STREAM, 8, 4, 99, 1),
+                (_lib.GEMM_K128, 16, 2, 1, 1), (7, 8, 4, 1, 1)]:
+        c = _lib.GemmCfg(*cfg)
+        assert L.nf4_gemm_ref_cfg(F, 1, F, 64 * 2048, F, 64 * 64, F, 16, F, _lib.BF16, 64, 4096, F, 1 << 30,
+                                  ctypes.byref(c), None) == _lib.ERR_ARG, cfg
+    # the streaming kernel needs K % 256 == 0
+    c = _lib.GemmCfg(_lib.GEMM_STREAM, 8, 4, 1, 1)
+    assert L.nf4_gemm_ref_cfg(F, 1, F, 64 * 64, F, 128, F, 1, F, _lib.BF16, 64, 128, F, 1 << 30,
+                              ctypes.byref(c), None) == _lib.ERR_ARG
