@@ -21,8 +21,9 @@ on the launch stream (region time / K: inter-launch gaps count against us);
 profiles/<round>/pmc_traffic.json (tools/pmc_traffic.py) when present.
 
 CPU baseline (``cpu_baseline``, rank 0 at N=1): the C oracle (scalar port of
-the reference fallback, 1 thread) on the same 4096x4096 workload, repeated for
-~--cpu-seconds.
+the reference fallback, rows split over OpenMP threads = this GPU's host share,
+at most 16) on the same 4096x4096 workload, repeated for ~--cpu-seconds; the
+1-thread figure is reported beside it (``single_thread``).
 
 Multi-GPU (weak scaling): every rank dequantizes its own matrices; rank 0 owns
 the quant statistics of all ranks' matrices and broadcasts them once over RCCL
@@ -81,23 +82,36 @@ def gen_stats(m, n, seed):
 
 
 def cpu_baseline(m, n, seconds, dtype_code):
-    """Time the scalar C oracle (1 thread) on the same workload for ~`seconds`."""
+    """Time the C oracle on the same workload: ~`seconds` with one thread per core of
+    this GPU's host share (rows split over OpenMP threads), then ~`seconds`/4 with
+    one thread (the scalar figure, reported alongside)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import nf4_oracle as O
 
     c = O.COracle()
     p, a1, a2 = O.make_inputs(m, n, 3409)
-    t0 = time.perf_counter()
-    reps = 0
-    while True:
-        c.dequant_ref(p, a1, a2, m, n, dtype_code)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": reps * m * n / el, "unit": "elements/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} x {m}x{n} NF4->bf16 dequant by oracle/nf4_oracle.c (scalar C, 1 thread), "
-                      f"{el:.1f} s"}
+
+    def timed(threads, secs):
+        c.set_threads(threads)
+        c.dequant_ref(p, a1, a2, m, n, dtype_code)  # warm (page-in, thread pool)
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            c.dequant_ref(p, a1, a2, m, n, dtype_code)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return reps, el
+
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
+    reps, el = timed(threads, seconds)
+    reps1, el1 = timed(1, max(1.0, seconds / 4))
+    c.set_threads(1)
+    return {"value": reps * m * n / el, "unit": "elements/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x {m}x{n} NF4->bf16 dequant by oracle/nf4_oracle.c (scalar C, rows over "
+                      f"{threads} OpenMP threads), {el:.1f} s",
+            "single_thread": {"value": reps1 * m * n / el1, "cores": 1,
+                              "sample": f"{reps1} x {m}x{n}, 1 thread, {el1:.1f} s"}}
 
 
 def main():

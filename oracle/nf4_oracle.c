@@ -103,6 +103,11 @@ float nf4o_ref_scale(const uint8_t* a1, int64_t nb, const float* a2, int64_t n2,
 /* One row-major [m, n] plane, scale per (row, block) supplied by `scale_of`. */
 typedef float (*scale_fn)(const void* ctx, int64_t r, int64_t b);
 
+/* Rows are independent, so the CPU-baseline form splits them over
+ * OpenMP threads; the arithmetic per element is identical for any thread count. */
+static int g_threads = 1;
+void nf4o_set_threads(int t) { g_threads = t < 1 ? 1 : t; }
+
 static int dequant_rows(const uint8_t* packed, int64_t packed_len, int64_t m, int64_t n,
                         void* out, int dtype, scale_fn sf, const void* ctx) {
     if (m <= 0 || n <= 0) return 0;
@@ -110,6 +115,7 @@ static int dequant_rows(const uint8_t* packed, int64_t packed_len, int64_t m, in
     int64_t stride = packed_len / m;
     if (stride < (n + 1) / 2) return -1;               /* row too short for n columns */
     int64_t bpr = (n + 63) / 64;
+#pragma omp parallel for num_threads(g_threads) schedule(static) if (g_threads > 1)
     for (int64_t r = 0; r < m; ++r) {
         const uint8_t* row = packed + r * stride;
         for (int64_t b = 0; b < bpr; ++b) {

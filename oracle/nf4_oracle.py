@@ -240,6 +240,8 @@ class COracle:
         i64, p = ctypes.c_int64, ctypes.c_void_p
         L = self.lib
         L.nf4o_dequant_ref.argtypes = [p, i64, p, i64, p, i64, p, ctypes.c_int, i64, i64]
+        L.nf4o_set_threads.argtypes = [ctypes.c_int]
+        L.nf4o_set_threads.restype = None
         L.nf4o_dequant_single.argtypes = [p, i64, p, i64, p, ctypes.c_int, i64, i64]
         L.nf4o_dequant_bnb.argtypes = [p, p, i64, p, p, i64, ctypes.c_float, p, ctypes.c_int, i64, i64, i64]
         L.nf4o_dequant_bnb_single.argtypes = [p, p, i64, p, ctypes.c_int, i64, i64]
@@ -253,6 +255,10 @@ class COracle:
     @staticmethod
     def _p(a):
         return a.ctypes.data_as(ctypes.c_void_p)
+
+    def set_threads(self, t: int) -> None:
+        """OpenMP threads for the row loop (CPU-baseline timing; results do not depend on it)."""
+        self.lib.nf4o_set_threads(int(t))
 
     def dequant_ref(self, packed, a1, a2, m, n, dtype):
         packed = np.ascontiguousarray(packed, np.uint8)

@@ -150,3 +150,15 @@ def test_fp32_output_is_unrounded(coracle):
     assert np.array_equal(got, want)
     bf = O.dequant_ref_np(p, a1, a2, 8, 128, O.BF16)
     assert np.array_equal(O.f32_to_bf16_bits(got), bf)
+
+
+def test_threaded_oracle_is_identical(coracle):
+    """The CPU-baseline form (rows over OpenMP threads) computes the same bits."""
+    p, a1, a2 = O.make_inputs(96, 448, 31)
+    one = coracle.dequant_ref(p, a1, a2, 96, 448, O.BF16)
+    coracle.set_threads(4)
+    try:
+        four = coracle.dequant_ref(p, a1, a2, 96, 448, O.BF16)
+    finally:
+        coracle.set_threads(1)
+    assert np.array_equal(one, four)

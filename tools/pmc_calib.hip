@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void calib_read_dword(const uint32_t* p, uint3
     if (acc == 0x9E3779B9u) sink[wave] = acc;  // practically never: keeps the loads alive
 }
 
-// Writes `nbytes` with 16 B/lane nt buffer stores, 1 KiB contiguous per wave
+// Writes `nbytes` with 16 B/lane sc1+nt buffer stores (the product default, aux 18), 1 KiB contiguous per wave
 // instruction (the output store shape).
 __global__ __launch_bounds__(256) void calib_write_x4(uint32_t* p, uint32_t nbytes) {
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, nbytes, 0x00020000);
@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void calib_write_x4(uint32_t* p, uint32_t nbyt
     const u32x4 v = {lane, wave, 1u, 2u};
     for (uint32_t base = wave * 8192u; base < nbytes; base += nw * 8192u) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_buffer_store_b128(v, r, base + 1024u * j + 16u * lane, 0, 2);
+        for (int j = 0; j < 8; ++j) __builtin_amdgcn_raw_buffer_store_b128(v, r, base + 1024u * j + 16u * lane, 0, 18);
     }
 }
 

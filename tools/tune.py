@@ -66,6 +66,15 @@ def main():
         assert rc == 0, rc
 
     stream = torch.cuda.current_stream()
+    ok = []
+    for c in cfgs:  # drop combinations the ABI rejects (NF4DQ_ERR_ARG)
+        q, a1, a2, out = sets[0]
+        rc = L.nf4_dequant_ref_cfg(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                                   out.data_ptr(), code, m, n, ctypes.byref(_lib.LaunchCfg(*c)),
+                                   stream.cuda_stream)
+        if rc == 0:
+            ok.append(c)
+    cfgs = ok
     res = {c: {"ev": [], "graph": []} for c in cfgs}
     graphs = {}
     for c in cfgs:
