@@ -146,7 +146,7 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
 
 /* Tuning form of nf4_gemm_ref.  kernel: 0 = library choice,
  * NF4DQ_GEMM_STREAM (K % 256 == 0; waves 4/8/16, depth = chunks in flight per
- * wave 2/4 (16 waves only when M <= 16), strips = 16-column strips per workgroup
+ * wave 2/4/8 (8 not with 16 waves; 16 waves only when M <= 16), strips = 16-column strips per workgroup
  * 1/2/4 dividing waves) or NF4DQ_GEMM_K128 (waves 4/8, depth 1/2/4 (<= 2 when
  * M > 16), strips ignored).  ksplit: K slices reduced across workgroups.
  * An invalid combination returns NF4DQ_ERR_ARG. */
@@ -164,6 +164,30 @@ int nf4_gemm_ref_cfg(const void* x, int64_t M, const uint8_t* packed, int64_t pa
                      const uint8_t* absmax_q, int64_t nb, const float* absmax2, int64_t n2,
                      void* y, int32_t out_dtype, int64_t N, int64_t K,
                      void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfg, void* hip_stream);
+
+/* Several weights that share the activation x (q/k/v, gate/up): one launch.
+ * Each weight: packed [N*K/2], its own absmax_q / absmax2 (reference wrap
+ * semantics per weight), output y [M][N] (out_dtype).  Same shape rules as
+ * nf4_gemm_ref for every weight (N % 64 == 0), at most NF4DQ_GEMM_GROUP_MAX
+ * weights; cfg NULL = library choice for the summed N (a configuration other
+ * than NF4DQ_GEMM_STREAM runs one launch per weight).  Workspace as for
+ * nf4_gemm_ref, sized by nf4_gemm_grouped_workspace_bytes. */
+#define NF4DQ_GEMM_GROUP_MAX 8
+typedef struct nf4_gemm_mat {
+    const uint8_t* packed;
+    int64_t packed_len;
+    const uint8_t* absmax_q;
+    int64_t nb;
+    const float* absmax2;
+    int64_t n2;
+    void* y;
+    int64_t N;
+} nf4_gemm_mat;
+size_t nf4_gemm_grouped_workspace_bytes(int64_t M, int64_t K, const nf4_gemm_mat* mats, int32_t count,
+                                        const nf4_gemm_cfg* cfg);
+int nf4_gemm_ref_grouped(const void* x, int64_t M, int64_t K, const nf4_gemm_mat* mats, int32_t count,
+                         int32_t out_dtype, void* workspace, size_t workspace_bytes,
+                         const nf4_gemm_cfg* cfg, void* hip_stream);
 
 /* Human-readable text for a return code (static storage). */
 const char* nf4_strerror(int code);

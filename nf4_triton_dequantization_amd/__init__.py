@@ -13,6 +13,7 @@ from .kernel import (  # noqa: F401
     dequantize_nf4_into,
     dequantize_nf4_many,
     nf4_linear,
+    nf4_linear_grouped,
     reset_triton_dequantize_state,
     triton_dequantize_nf4,
 )
@@ -20,6 +21,6 @@ from .bnb_layout import Linear4bit, Params4bit, QuantState, quantize_nf4  # noqa
 from .checkpoint import load_nf4_safetensors, save_nf4_safetensors  # noqa: F401
 
 __all__ = ["triton_dequantize_nf4", "reset_triton_dequantize_state", "dequantize_nf4_many",
-           "dequantize_nf4_bnb", "dequantize_nf4_into", "nf4_linear", "Linear4bit", "Params4bit", "QuantState",
-           "quantize_nf4", "load_nf4_safetensors", "save_nf4_safetensors"]
+           "dequantize_nf4_bnb", "dequantize_nf4_into", "nf4_linear", "nf4_linear_grouped", "Linear4bit",
+           "Params4bit", "QuantState", "quantize_nf4", "load_nf4_safetensors", "save_nf4_safetensors"]
 __version__ = "0.1.0"

@@ -63,6 +63,17 @@ GEMM_K128 = 1
 GEMM_STREAM = 2
 
 
+GEMM_GROUP_MAX = 8
+
+
+class GemmMat(ctypes.Structure):
+    """nf4_gemm_mat (include/nf4_dequant.h)."""
+
+    _fields_ = [("packed", ctypes.c_void_p), ("packed_len", ctypes.c_int64), ("absmax_q", ctypes.c_void_p),
+                ("nb", ctypes.c_int64), ("absmax2", ctypes.c_void_p), ("n2", ctypes.c_int64),
+                ("y", ctypes.c_void_p), ("N", ctypes.c_int64)]
+
+
 class GemmCfg(ctypes.Structure):
     """nf4_gemm_cfg (include/nf4_dequant.h)."""
 
@@ -86,6 +97,10 @@ SIGNATURES = {
     "nf4_gemm_workspace_bytes_cfg": (ctypes.c_size_t, [_I64, _I64, _I64, ctypes.POINTER(GemmCfg)]),
     "nf4_gemm_ref_cfg": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I32, _I64, _I64, _P,
                                         ctypes.c_size_t, ctypes.POINTER(GemmCfg), _P]),
+    "nf4_gemm_grouped_workspace_bytes": (ctypes.c_size_t, [_I64, _I64, ctypes.POINTER(GemmMat), _I32,
+                                                           ctypes.POINTER(GemmCfg)]),
+    "nf4_gemm_ref_grouped": (ctypes.c_int, [_P, _I64, _I64, ctypes.POINTER(GemmMat), _I32, _I32, _P, ctypes.c_size_t,
+                                            ctypes.POINTER(GemmCfg), _P]),
     "nf4_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "nf4_version": (ctypes.c_char_p, []),
 }

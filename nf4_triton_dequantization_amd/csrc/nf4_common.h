@@ -57,17 +57,28 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
     }
 }
 
-// The 16 NF4 code points (fp32 bit patterns of kernel_optimized.py:234-239)
-// into LDS from immediates (no global load on the
-// kernel's critical path): thread 0 writes four 16-byte rows.
+// The 16 NF4 code points: fp32 bit patterns of kernel_optimized.py:234-239.
+constexpr uint32_t kNf4Bits[16] = {0xbf800000u, 0xbf3239b1u, 0xbf066b30u, 0xbeca32a0u, 0xbe91a24du, 0xbe3d353fu,
+                                   0xbdba7871u, 0x00000000u, 0x3da2faffu, 0x3e24cae3u, 0x3e7c04ddu, 0x3ead033au,
+                                   0x3ee1a4b8u, 0x3f1007abu, 0x3f3913b3u, 0x3f800000u};
+
+// The code table into LDS from immediates (no global load on the kernel's
+// critical path): thread 0 writes four 16-byte rows.
 __device__ __forceinline__ void write_lut(float* lut) {
     if (threadIdx.x == 0) {
         u32x4* l4 = reinterpret_cast<u32x4*>(lut);
-        l4[0] = u32x4{0xbf800000u, 0xbf3239b1u, 0xbf066b30u, 0xbeca32a0u};
-        l4[1] = u32x4{0xbe91a24du, 0xbe3d353fu, 0xbdba7871u, 0x00000000u};
-        l4[2] = u32x4{0x3da2faffu, 0x3e24cae3u, 0x3e7c04ddu, 0x3ead033au};
-        l4[3] = u32x4{0x3ee1a4b8u, 0x3f1007abu, 0x3f3913b3u, 0x3f800000u};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            l4[r] = u32x4{kNf4Bits[4 * r], kNf4Bits[4 * r + 1], kNf4Bits[4 * r + 2], kNf4Bits[4 * r + 3]};
     }
+}
+
+// Code point i: a constant for constant i, a select chain otherwise.
+__device__ __forceinline__ float nf4_code(uint32_t i) {
+    uint32_t v = kNf4Bits[0];
+#pragma unroll
+    for (uint32_t j = 1; j < 16; ++j) v = i == j ? kNf4Bits[j] : v;
+    return __uint_as_float(v);
 }
 
 // Buffer-resource flags word (raw buffer, dword format) for gfx950.

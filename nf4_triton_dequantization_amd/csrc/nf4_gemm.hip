@@ -9,18 +9,19 @@
 // once (0.5 B/element) and dequantized in registers -- the roofline is HBM on
 // the packed weight, not on a 2 B/element bf16 copy.
 //
-// Decomposition: a wave owns 16 output columns (one MFMA 16x16x32 column tile)
-// over a K slice; a 4-wave workgroup owns 64 adjacent columns of one K slice.
-// Per 128-deep K chunk a lane loads 16 packed bytes of its weight row
-// (row n0 + (lane & 15), k = 128c + 32(lane >> 4) .. +32: one 64-block, one
-// scale) and the matching 64 bytes of each activation row; packed dword s of
-// the lane is exactly the MFMA B fragment of step s (k = 8s + j inside the
-// lane's 32) and activation bytes [16s, 16s+16) its A fragment -- the same k
-// permutation on both operands, so no shuffle is needed.  Chunks are
-// software-pipelined two deep (register sets P/Q).  K slices > 1 write fp32
-// partials to a workspace slab; the last workgroup to finish a column group
-// (ticket counter) sums the slices in slice order and writes y -- one launch,
-// bitwise reproducible, no float atomics.
+// Two kernels (host choice in default_gemm_cfg, explicit in nf4_gemm_ref_cfg):
+//  * nf4_gemm_smallm_kernel -- K % 128 == 0; 128-deep chunks, a lane loads 16
+//    packed bytes of its weight row (one 64-block, one scale) and the matching
+//    activation fragments from global memory; waves of a workgroup split K and
+//    meet in LDS.
+//  * nf4_gemm_stream_kernel -- K % 256 == 0 (every Llama shape); 256-deep
+//    chunks (one 128-byte line per weight row), activations staged in LDS,
+//    a register ring of weight chunks, pair-table dequant (see its comments).
+// Both use the same k permutation on A and B fragments (a lane's packed dword
+// is exactly its MFMA B fragment of one step), so no shuffle is needed.  K
+// slices over workgroups (ksplit > 1) write fp32 partials to a workspace slab;
+// the last workgroup to finish a column strip (ticket counter) sums the slices
+// in slice order and writes y -- one launch, bitwise reproducible, no float atomics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -239,23 +240,35 @@ constexpr uint32_t kSChunkK = 256;
 constexpr int kXR = 8;               // x staging: 16-byte pieces per thread and row tile
 constexpr uint32_t kLdsX = 0;        // dynamic LDS: [x slice][zero block][partials]
 
-struct StreamArgs {
+// One weight of a launch.  Several weights that share x (q/k/v, gate/up) go in
+// one launch: workgroups are numbered over all their strip groups.
+constexpr int kGroupMax = 8;
+struct StreamMat {
     const uint8_t* packed;
     const uint8_t* a1;
     const float* a2;
+    void* y;                // [M][N]
+    uint32_t N;
+    uint32_t sg_begin;      // first strip group of this weight in the launch
+    uint32_t strip_begin;   // first 16-column strip (ticket counters), = col_begin / 16
+    uint32_t nb_bytes, n2_bytes;
+    FastDiv nb, n2;
+};
+
+struct StreamArgs {
+    StreamMat mat[kGroupMax];
+    uint32_t nmat;
+    uint32_t sg_total;      // strip groups over all weights
+    uint32_t ncols;         // sum of N (split-K slab row length)
     const void* x;
-    void* y;
     float* slab;
     uint32_t* counters;
-    uint32_t M, N, K;
-    uint32_t strip_groups;  // N / (16 T)
+    uint32_t M, K;
     uint32_t T, parts;      // strips per workgroup, K parts per strip
     uint32_t ksplit, cps;   // K slices, chunks per slice
     uint32_t cpp;           // chunks per K part (a part's chunks are contiguous)
     uint32_t chunks;        // K / 256
     uint32_t bpr, groups;   // K / 64, ceil(bpr / 4)
-    uint32_t nb_bytes, n2_bytes;
-    FastDiv nb, n2;
     FastDiv ppr;            // 16-byte x pieces per staged row (cps * 32)
     uint32_t xstride;       // LDS bytes per staged x row
     uint32_t zero_off;      // 128 zero bytes: the A operand of rows >= M
@@ -292,10 +305,11 @@ struct SSlot {
 #define NF4_STREAM_DEBUG 0
 #endif
 
-constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads return 0, no traffic
+constexpr uint32_t kOob = 0x80000000u;
+constexpr int kVsMax = 16;  // chunks per wave covered by the vector-scale form  // beyond every buffer range: loads return 0, no traffic
 
-template <bool VS, class Args>
-__device__ __forceinline__ void sslot_issue(const Args& A, __amdgpu_buffer_rsrc_t rw,
+template <bool VS>
+__device__ __forceinline__ void sslot_issue(const StreamArgs& A, const StreamMat& Mt, __amdgpu_buffer_rsrc_t rw,
                                             __amdgpu_buffer_rsrc_t ra1, __amdgpu_buffer_rsrc_t ra2, uint32_t c,
                                             bool valid, uint32_t row, uint32_t kh, SSlot& s) {
     // `valid` is wave-uniform; past the wave's last chunk the offsets get bit 31
@@ -315,8 +329,8 @@ __device__ __forceinline__ void sslot_issue(const Args& A, __amdgpu_buffer_rsrc_
     s.w1 = __builtin_amdgcn_raw_buffer_load_b128(rw, woff + 16u, 0, 0);
     if constexpr (!VS) {
         // block 4c + kh of the row; its nested group is c (reference wraps, :173-186)
-        const uint32_t i1 = fmodu(row * A.bpr + 4u * c + kh, A.nb) | oob;
-        const uint32_t i2 = (fmodu(row * A.groups + c, A.n2) * 4u) | oob;
+        const uint32_t i1 = fmodu(row * A.bpr + 4u * c + kh, Mt.nb) | oob;
+        const uint32_t i2 = (fmodu(row * A.groups + c, Mt.n2) * 4u) | oob;
 #if NF4_STREAM_DEBUG == 4
         s.qa = i1 & 0xFFu;
         s.qb = __uint_as_float(i2 & 0x3FFFFFFFu);
@@ -340,46 +354,69 @@ __device__ __forceinline__ void sslot_mma(const SSlot& s, uint32_t qa, float qb,
                                           const float* qtab, const char* smem, uint32_t slot8,
                                           const uint32_t (&xa)[MT], f32x4 (&acc)[MT]) {
     const float sc = qtab[qa] * qb;  // (:45, :97-98)
-    const f32x2 sc2 = {sc, sc};
+    // both halves materialised: a half left to op_sel would read a stale
+    // register, and its pending load (as far as the waitcnt pass knows) drains the ring
+    const f32x2 sc2 = {sc, opaque(sc)};
     const char* pt = reinterpret_cast<const char*>(ptab);
-#pragma unroll
-    for (int st = 0; st < 8; ++st) {
+    // Pair lookups run LA steps ahead of their use (one LDS round trip per chunk,
+    // not one per MFMA step): 4 x LA reads in flight, counted lgkmcnt waits.
+    constexpr int LA = 3;
+    f32x2 v[8][4];
+    auto issue = [&](int st) {
         const uint32_t wd = st < 4 ? s.w0[st] : s.w1[st - 4];
-        uint32_t bw[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const uint32_t addr = __builtin_amdgcn_perm(wd, slot8, 0x0C0C0000u | ((4u + b) << 8));
-            const f32x2 v = *reinterpret_cast<const f32x2*>(pt + addr) * sc2;  // fp32 products (:97-98)
-            bw[b] = pack2<DT>(v.x, v.y);                                         // RNE (:109-110)
+            v[st][b] = *reinterpret_cast<const f32x2*>(pt + addr);
+        }
+    };
+#pragma unroll
+    for (int st = 0; st < LA; ++st) issue(st);
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+        if (st + LA < 8) issue(st + LA);
+        u32x4 a[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) a[mt] = *reinterpret_cast<const u32x4*>(smem + xa[mt] + 16u * st);
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t bw[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const f32x2 p = v[st][b] * sc2;  // fp32 products (:97-98)
+            bw[b] = pack2<DT>(p.x, p.y);     // RNE (:109-110)
         }
         const u32x4 bq = {bw[0], bw[1], bw[2], bw[3]};
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-            const u32x4 a = *reinterpret_cast<const u32x4*>(smem + xa[mt] + 16u * st);
             if constexpr (DT == NF4DQ_BF16) {
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[mt]),
                                                                   __builtin_bit_cast(bf16x8, bq), acc[mt], 0, 0, 0);
             } else {
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[mt]),
                                                                  __builtin_bit_cast(f16x8, bq), acc[mt], 0, 0, 0);
             }
         }
     }
 }
 
-// VS: vector scales -- no absmax wrap (nb >= N K / 64, n2 >= N groups) and a
-// wave's chunks all in its ring (cpp <= P): its 4 x 4 absmax bytes and 4
-// nested scales come in two 16-byte loads up front instead of two gathers per chunk.
+// VS: vector scales -- no absmax wrap inside a row (nb a multiple of K / 64 or
+// >= N K / 64, n2 a multiple of groups or >= N groups: true for every real
+// bitsandbytes state, where n2 = N groups / 64) and at most kVsMax chunks per wave: the wave's absmax bytes (4 per chunk) and nested
+// scales (1 per chunk) come in 16-byte loads up front instead of two gathers
+// per chunk, and the chunk loop is unrolled so that every index is static.
 template <int DT, int MT, int W, int P, bool VS>
 __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArgs A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ __attribute__((aligned(16))) f32x2 ptab[256 * 32];  // 64 KiB pair table, built per workgroup
-    __shared__ __attribute__((aligned(16))) float lut[16];
     __shared__ float qtab[256];
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar control flow below
     const uint32_t nl = lane & 15u, kh = lane >> 4;
-    const uint32_t sg = blockIdx.x % A.strip_groups, ks = blockIdx.x / A.strip_groups;
+    const uint32_t sgi = blockIdx.x % A.sg_total, ks = blockIdx.x / A.sg_total;
+    uint32_t mi = 0;  // the weight this workgroup works on (uniform scan)
+    for (uint32_t i = 1; i < A.nmat; ++i) mi = sgi >= A.mat[i].sg_begin ? i : mi;
+    const StreamMat& Mt = A.mat[mi];
+    const uint32_t sg = sgi - Mt.sg_begin;
     const uint32_t strip = sg * A.T + wave % A.T, part = wave / A.T;
     const uint32_t row = strip * 16u + nl;
     const uint32_t s0 = ks * A.cps;
@@ -399,9 +436,9 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     }
 #endif
 
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.N * (A.K >> 1), kRsrcFlags);
-    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)A.a1, 0, A.nb_bytes, kRsrcFlags);
-    const __amdgpu_buffer_rsrc_t ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)A.a2, 0, A.n2_bytes, kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a1, 0, Mt.nb_bytes, kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a2, 0, Mt.n2_bytes, kRsrcFlags);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
 
     // 1. activation slice loads first (the counted waits below then leave the weight ring in flight)
@@ -420,34 +457,41 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     // 2. the weight ring (VS: the wave's scales first)
     // (issue order = the loop's: slot by slot, w0 w1 qa qb -- the scheduler must
     // not regroup them, or the waitcnt pass merges two orders into a drain)
-    u32x4 a1v = {0u, 0u, 0u, 0u};
-    u32x4 a2v = {0u, 0u, 0u, 0u};
+    constexpr int NV = VS ? kVsMax / 4 : 1;
+    u32x4 a1v[NV], a2v[NV];
     if constexpr (VS) {
         const uint32_t cf = s0 + l0;
-        const uint32_t oob = cnt ? 0u : kOob;
-        a1v = __builtin_amdgcn_raw_buffer_load_b128(ra1, (row * A.bpr + 4u * cf) | oob, 0, 0);
-        a2v = __builtin_amdgcn_raw_buffer_load_b128(ra2, ((row * A.groups + cf) * 4u) | oob, 0, 0);
+        // the row's wrapped bases (reference repeat semantics, :173-186); no wrap inside the row
+        const uint32_t b1 = fmodu(row * A.bpr, Mt.nb) + 4u * cf;
+        const uint32_t b2 = fmodu(row * A.groups, Mt.n2) + cf;
+#pragma unroll
+        for (int g = 0; g < NV; ++g) {
+            const uint32_t oob = 4u * g < cnt ? 0u : kOob;  // groups past the wave's range: no traffic
+            a1v[g] = __builtin_amdgcn_raw_buffer_load_b128(ra1, (b1 + 16u * g) | oob, 0, 0);
+            a2v[g] = __builtin_amdgcn_raw_buffer_load_b128(ra2, ((b2 + 4u * g) * 4u) | oob, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
     SSlot ring[P];
 #pragma unroll
     for (int j = 0; j < P; ++j) {
-        sslot_issue<VS>(A, rw, ra1, ra2, s0 + l0 + (uint32_t)j, (uint32_t)j < cnt, row, kh, ring[j]);
+        sslot_issue<VS>(A, Mt, rw, ra1, ra2, s0 + l0 + (uint32_t)j, (uint32_t)j < cnt, row, kh, ring[j]);
         __builtin_amdgcn_sched_barrier(0);
     }
-    // 3. tables, then the staged slice (waits for the x loads only)
-    write_lut(lut);
+    // 3. tables (no global data: they fill while the loads fly), then the staged
+    // slice (waits for the x loads only), one barrier.  Pair table: entry
+    // e = 16 hi + lo of lane slot t at byte 256 e + 8 t; a thread owns one
+    // (lo, t) and writes it for all 16 hi -- the hi codes are immediates.
     if (tid < 256u) qtab[tid] = (float)tid / 127.0f;  // IEEE division
     if (tid < 8u) *reinterpret_cast<u32x4*>(smem + A.zero_off + 16u * tid) = u32x4{0u, 0u, 0u, 0u};
+    for (uint32_t u = tid; u < 16u * 32u; u += 64u * W) {
+        const float clo = nf4_code(u >> 5);
+#pragma unroll
+        for (int hi = 0; hi < 16; ++hi) ptab[(16u * hi + (u >> 5)) * 32u + (u & 31u)] = f32x2{nf4_code(hi), clo};
+    }
 #pragma unroll
     for (int i = 0; i < XR; ++i)
         if (xdst[i] != 0xFFFFFFFFu) *reinterpret_cast<u32x4*>(smem + xdst[i]) = xv[i];
-    __syncthreads();
-    // the pair table: entry e of lane slot t at byte 256 e + 8 t
-    for (uint32_t i = tid; i < 256u * 32u; i += 64u * W) {
-        const uint32_t e = i >> 5;
-        ptab[i] = f32x2{lut[e >> 4], lut[e & 15u]};
-    }
     __syncthreads();
     NF4_STAMP(1);
 #if NF4_STREAM_DEBUG == 3
@@ -465,30 +509,44 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (uint32_t base = 0; base < cnt; base += P) {
+    auto body = [&](uint32_t jj, int j, uint32_t qa, float qb) {
+        const uint32_t l = l0 + jj;  // chunk within the slice
+        uint32_t xa[MT];
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const uint32_t jj = base + (uint32_t)j;
-            if (jj < cnt) {
-                const uint32_t l = l0 + jj;  // chunk within the slice
-                uint32_t xa[MT];
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) xa[mt] = live[mt] ? xa0[mt] + l * 512u : xa0[mt];
-                // VS: cnt <= P, so jj == j here and the vector lanes are static
-                const uint32_t qa = VS ? (a1v[j] >> (8u * kh)) & 0xFFu : ring[j].qa;
-                const float qb = VS ? __uint_as_float(a2v[j]) : ring[j].qb;
+        for (int mt = 0; mt < MT; ++mt) xa[mt] = live[mt] ? xa0[mt] + l * 512u : xa0[mt];
 #if NF4_STREAM_DEBUG == 1 || NF4_STREAM_DEBUG == 4 || NF4_STREAM_DEBUG == 5
-                acc[0][0] += __uint_as_float((ring[j].w0[0] ^ ring[j].w1[3] ^ qa) & 0x3FFFFFFFu) * qb;
-                (void)xa;
+        acc[0][0] += __uint_as_float((ring[j].w0[0] ^ ring[j].w1[3] ^ qa) & 0x3FFFFFFFu) * qb;
+        (void)xa;
 #else
-                sslot_mma<DT, MT>(ring[j], qa, qb, ptab, qtab, smem, slot8, xa, acc);
+        sslot_mma<DT, MT>(ring[j], qa, qb, ptab, qtab, smem, slot8, xa, acc);
 #endif
+    };
+    if constexpr (VS) {
+        // fully unrolled: ring slot jj % P, scale lanes jj / 4 and jj % 4 are static
+#pragma unroll
+        for (int jj = 0; jj < kVsMax; ++jj) {
+            const int j = jj % P;
+            if ((uint32_t)jj < cnt)  // uniform
+                body((uint32_t)jj, j, (a1v[jj / 4][jj % 4] >> (8u * kh)) & 0xFFu,
+                     __uint_as_float(a2v[jj / 4][jj % 4]));
+            __builtin_amdgcn_sched_barrier(0);
+            // unconditional (past the range: out-of-range offsets, no traffic), so
+            // both sides of the guard leave the same loads pending
+            const uint32_t jn = (uint32_t)jj + P;
+            sslot_issue<VS>(A, Mt, rw, ra1, ra2, s0 + l0 + jn, jn < cnt, row, kh, ring[j]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        for (uint32_t base = 0; base < cnt; base += P) {
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const uint32_t jj = base + (uint32_t)j;
+                if (jj < cnt) body(jj, j, ring[j].qa, ring[j].qb);
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t jn = jj + P;
+                sslot_issue<VS>(A, Mt, rw, ra1, ra2, s0 + l0 + jn, jn < cnt, row, kh, ring[j]);
+                __builtin_amdgcn_sched_barrier(0);
             }
-            __builtin_amdgcn_sched_barrier(0);
-            if (VS) continue;  // the whole range is in the ring already
-            const uint32_t jn = jj + P;
-            sslot_issue<VS>(A, rw, ra1, ra2, s0 + l0 + jn, jn < cnt, row, kh, ring[j]);
-            __builtin_amdgcn_sched_barrier(0);
         }
     }
 
@@ -514,46 +572,47 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint32_t m = 16u * mt + 4u * kh + r;
-                if (m < A.M) store_y<DT>(A.y, m * A.N + row, acc[mt][r]);
+                if (m < A.M) store_y<DT>(Mt.y, m * Mt.N + row, acc[mt][r]);
             }
         NF4_STAMP(3);
         return;
     }
     // 5. split-K across workgroups: the hand-off of nf4_gemm_smallm_kernel, per strip
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)A.slab, 0, A.ksplit * A.M * A.N * 4u, kRsrcFlags);
+        (void*)A.slab, 0, A.ksplit * A.M * A.ncols * 4u, kRsrcFlags);
+    const uint32_t gstrip = Mt.strip_begin + strip;  // launch-wide strip: counter and slab column
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t m = 16u * mt + 4u * kh + r;
-            const uint32_t off = m < A.M ? ((ks * A.M + m) * A.N + row) * 4u : kOob;
+            const uint32_t off = m < A.M ? ((ks * A.M + m) * A.ncols + gstrip * 16u + nl) * 4u : kOob;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][r]), rs, off, 0, kAuxSc1);
         }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t last = 0;
     if (lane == 0) {
-        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[strip], 1u, __ATOMIC_RELAXED,
+        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[gstrip], 1u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT);
         last = ticket == A.ksplit - 1u;
-        if (last) __hip_atomic_store(&A.counters[strip], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (last) __hip_atomic_store(&A.counters[gstrip], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
     for (uint32_t i = lane; i < A.M * 16u; i += 64u) {
         const uint32_t m = i >> 4;
-        const uint32_t n = strip * 16u + (i & 15u);
+        const uint32_t c = i & 15u;
         float sum = 0.0f;
         for (uint32_t k = 0; k < A.ksplit; ++k)
-            sum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ((k * A.M + m) * A.N + n) * 4u, 0, kAuxSc1));
-        store_y<DT>(A.y, m * A.N + n, sum);
+            sum += __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(rs, ((k * A.M + m) * A.ncols + gstrip * 16u + c) * 4u, 0, kAuxSc1));
+        store_y<DT>(Mt.y, m * Mt.N + strip * 16u + c, sum);
     }
 }
 
-
 // ---- decomposition choice --------------------------------------------------
 constexpr uint32_t kLdsPerCu = 160 * 1024;
-constexpr uint32_t kStreamStatic = 256 * 32 * 8 + 64 + 1024;  // pair table, code LUT, q/127 table
+constexpr uint32_t kStreamStatic = 256 * 32 * 8 + 1024;  // pair table, q/127 table
 constexpr uint32_t kStreamLdsCap = kLdsPerCu - kStreamStatic;  // dynamic part
 
 struct StreamPlan {
@@ -600,8 +659,8 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
     if (c.kernel == NF4DQ_GEMM_STREAM) {
         if (K % kSChunkK) return false;
         if (c.waves != 4 && c.waves != 8 && c.waves != 16) return false;
-        if (c.depth != 2 && c.depth != 4) return false;
-        if (c.waves == 16 && M > 16) return false;
+        if (c.depth != 2 && c.depth != 4 && c.depth != 8) return false;
+        if (c.waves == 16 && (M > 16 || c.depth == 8)) return false;
         if (c.strips != 1 && c.strips != 2 && c.strips != 4) return false;
         if (c.waves % c.strips || N % (16 * c.strips)) return false;
         if (c.ksplit < 1 || c.ksplit > K / kSChunkK) return false;
@@ -628,6 +687,114 @@ static size_t workspace_for(int64_t M, int64_t N, int64_t K, const nf4_gemm_cfg&
     return c.ksplit > 1 ? counters_bytes(N) + (size_t)c.ksplit * (size_t)M * (size_t)N * sizeof(float) : 0;
 }
 
+struct HostMat {
+    const uint8_t* packed;
+    int64_t packed_len;
+    const uint8_t* a1;
+    int64_t nb;
+    const float* a2;
+    int64_t n2;
+    void* y;
+    int64_t N;
+};
+
+// One launch of the streaming kernel over `count` weights sharing x (shapes and
+// cfg already validated; workspace = counters + ksplit * M * sum(N) fp32).
+static int launch_stream(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
+                         const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st) {
+    const StreamPlan pl = stream_plan(M, K, cfg);
+    const uint32_t ks = (uint32_t)cfg.ksplit;
+    StreamArgs S{};
+    S.nmat = (uint32_t)count;
+    S.x = x;
+    S.counters = reinterpret_cast<uint32_t*>(workspace);
+    S.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    S.M = (uint32_t)M;
+    S.K = (uint32_t)K;
+    S.T = (uint32_t)cfg.strips;
+    S.parts = (uint32_t)(cfg.waves / cfg.strips);
+    S.ksplit = ks;
+    S.chunks = (uint32_t)(K / kSChunkK);
+    S.cps = pl.cps;
+    S.cpp = (pl.cps + S.parts - 1) / S.parts;
+    S.bpr = (uint32_t)(K / 64);
+    S.groups = (S.bpr + 3) / 4;
+    S.ppr = make_fastdiv(pl.cps * 32u);
+    S.xstride = pl.xstride;
+    S.zero_off = pl.zero_off;
+    S.red_off = pl.red_off;
+#if NF4_STREAM_DEBUG == 3
+    S.stamps = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + kCounterBytes);
+#endif
+    // vector scales: no absmax wrap inside any row of any weight, and each wave's chunks <= kVsMax
+    bool vs = S.cpp <= (uint32_t)kVsMax;
+    uint32_t sg = 0, strips = 0;
+    for (int i = 0; i < count; ++i) {
+        const HostMat& h = mats[i];
+        StreamMat& m = S.mat[i];
+        m.packed = h.packed;
+        m.a1 = h.a1;
+        m.a2 = h.a2;
+        m.y = h.y;
+        m.N = (uint32_t)h.N;
+        m.sg_begin = sg;
+        m.strip_begin = strips;
+        const int64_t nbc = h.nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : h.nb;
+        const int64_t n2c = h.n2 > (int64_t(1) << 29) ? (int64_t(1) << 29) : h.n2;
+        m.nb = make_fastdiv((uint32_t)nbc);
+        m.n2 = make_fastdiv((uint32_t)n2c);
+        m.nb_bytes = (uint32_t)nbc;
+        m.n2_bytes = (uint32_t)(n2c * 4);
+        sg += (uint32_t)(h.N / (16 * cfg.strips));
+        strips += (uint32_t)(h.N / 16);
+        vs = vs && (h.nb % (K / 64) == 0 || h.nb >= h.N * (K / 64)) &&
+             (h.n2 % (int64_t)S.groups == 0 || h.n2 >= h.N * (int64_t)S.groups);
+    }
+    S.sg_total = sg;
+    S.ncols = strips * 16u;
+    const dim3 grid(sg * ks), block(64 * cfg.waves);
+    const int mt = (int)((M + 15) / 16);
+#define NF4_K1(DT_, MT_, W_, P_, VS_)                                                                       \
+    do {                                                                                                    \
+        static bool attr_ = false; /* static + dynamic LDS above 64 KiB needs the opt-in */                  \
+        if (!attr_) {                                                                                       \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_stream_kernel<DT_, MT_, W_, P_, VS_>), \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsCap);      \
+            attr_ = true;                                                                                   \
+        }                                                                                                   \
+        hipLaunchKernelGGL((nf4_gemm_stream_kernel<DT_, MT_, W_, P_, VS_>), grid, block, pl.lds, st, S);    \
+    } while (0)
+#define NF4_K(DT_, MT_, W_, P_)                 \
+    do {                                        \
+        if (vs) NF4_K1(DT_, MT_, W_, P_, true); \
+        else NF4_K1(DT_, MT_, W_, P_, false);   \
+    } while (0)
+#define NF4_P(DT_, MT_, W_)                                \
+    do {                                                   \
+        if (cfg.depth == 2) NF4_K(DT_, MT_, W_, 2);        \
+        else if (cfg.depth == 4) NF4_K(DT_, MT_, W_, 4);   \
+        else NF4_K(DT_, MT_, W_, (W_ == 16 ? 4 : 8));      \
+    } while (0)
+#define NF4_WW(DT_)                                        \
+    do {                                                   \
+        if (mt == 1) {                                     \
+            if (cfg.waves == 4) NF4_P(DT_, 1, 4);          \
+            else if (cfg.waves == 8) NF4_P(DT_, 1, 8);     \
+            else NF4_P(DT_, 1, 16);                        \
+        } else { /* 16 waves only for M <= 16 */           \
+            if (cfg.waves == 4) NF4_P(DT_, 2, 4);          \
+            else NF4_P(DT_, 2, 8);                         \
+        }                                                  \
+    } while (0)
+    if (dtype == NF4DQ_BF16) NF4_WW(NF4DQ_BF16);
+    else NF4_WW(NF4DQ_F16);
+#undef NF4_WW
+#undef NF4_P
+#undef NF4_K
+#undef NF4_K1
+    return hip_rc2(hipGetLastError());
+}
+
 static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,
                      int64_t nb, const float* absmax2, int64_t n2, void* y, int32_t dtype, int64_t N, int64_t K,
                      void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfgp, hipStream_t st) {
@@ -648,82 +815,8 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     const size_t need = workspace_for(M, N, K, cfg);
     if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
     if (cfg.kernel == NF4DQ_GEMM_STREAM) {
-        const StreamPlan pl = stream_plan(M, K, cfg);
-        StreamArgs S{};
-        S.packed = packed;
-        S.a1 = absmax_q;
-        S.a2 = absmax2;
-        S.x = x;
-        S.y = y;
-        S.counters = reinterpret_cast<uint32_t*>(workspace);
-        S.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + counters_bytes(N)) : nullptr;
-        S.M = (uint32_t)M;
-        S.N = (uint32_t)N;
-        S.K = (uint32_t)K;
-        S.T = (uint32_t)cfg.strips;
-        S.parts = (uint32_t)(cfg.waves / cfg.strips);
-        S.strip_groups = (uint32_t)(N / (16 * cfg.strips));
-        S.ksplit = ks;
-        S.chunks = (uint32_t)(K / kSChunkK);
-        S.cps = pl.cps;
-        S.bpr = (uint32_t)(K / 64);
-        S.groups = (S.bpr + 3) / 4;
-        const int64_t nbc = nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : nb;
-        const int64_t n2c = n2 > (int64_t(1) << 29) ? (int64_t(1) << 29) : n2;
-        S.nb = make_fastdiv((uint32_t)nbc);
-        S.n2 = make_fastdiv((uint32_t)n2c);
-        S.nb_bytes = (uint32_t)nbc;
-        S.n2_bytes = (uint32_t)(n2c * 4);
-        S.ppr = make_fastdiv(pl.cps * 32u);
-        S.xstride = pl.xstride;
-        S.zero_off = pl.zero_off;
-        S.red_off = pl.red_off;
-#if NF4_STREAM_DEBUG == 3
-        S.stamps = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + kCounterBytes);
-#endif
-        S.cpp = (pl.cps + S.parts - 1) / S.parts;
-        // vector scales: no absmax wrap anywhere in the matrix, and each wave's chunks fit its ring
-        const bool vs = nb >= N * (K / 64) && n2 >= N * (int64_t)S.groups && S.cpp <= (uint32_t)cfg.depth;
-        const dim3 grid(S.strip_groups * ks), block(64 * cfg.waves);
-        const int mt = (int)((M + 15) / 16);
-#define NF4_K1(DT_, MT_, W_, P_, VS_)                                                                       \
-    do {                                                                                                    \
-        static bool attr_ = false; /* static + dynamic LDS above 64 KiB needs the opt-in */                  \
-        if (!attr_) {                                                                                       \
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_stream_kernel<DT_, MT_, W_, P_, VS_>), \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsCap);      \
-            attr_ = true;                                                                                   \
-        }                                                                                                   \
-        hipLaunchKernelGGL((nf4_gemm_stream_kernel<DT_, MT_, W_, P_, VS_>), grid, block, pl.lds, st, S);    \
-    } while (0)
-#define NF4_K(DT_, MT_, W_, P_)                 \
-    do {                                        \
-        if (vs) NF4_K1(DT_, MT_, W_, P_, true); \
-        else NF4_K1(DT_, MT_, W_, P_, false);   \
-    } while (0)
-#define NF4_P(DT_, MT_, W_)                                \
-    do {                                                   \
-        if (cfg.depth == 2) NF4_K(DT_, MT_, W_, 2);        \
-        else NF4_K(DT_, MT_, W_, 4);                       \
-    } while (0)
-#define NF4_WW(DT_)                                        \
-    do {                                                   \
-        if (mt == 1) {                                     \
-            if (cfg.waves == 4) NF4_P(DT_, 1, 4);          \
-            else if (cfg.waves == 8) NF4_P(DT_, 1, 8);     \
-            else NF4_P(DT_, 1, 16);                        \
-        } else { /* 16 waves only for M <= 16 */           \
-            if (cfg.waves == 4) NF4_P(DT_, 2, 4);          \
-            else NF4_P(DT_, 2, 8);                         \
-        }                                                  \
-    } while (0)
-        if (dtype == NF4DQ_BF16) NF4_WW(NF4DQ_BF16);
-        else NF4_WW(NF4DQ_F16);
-#undef NF4_WW
-#undef NF4_P
-#undef NF4_K
-#undef NF4_K1
-        return hip_rc2(hipGetLastError());
+        const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
+        return launch_stream(&h, 1, x, M, K, dtype, cfg, workspace, st);
     }
     GemmArgs A{};
     A.packed = packed;
@@ -771,6 +864,75 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     return hip_rc2(hipGetLastError());
 }
 
+// Weights that share x, one launch when the streaming kernel applies; otherwise
+// one nf4_gemm_ref-equivalent launch per weight (same workspace, sequential on st).
+static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm_mat* mats, int32_t count,
+                             int32_t dtype, void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfgp,
+                             hipStream_t st) {
+    if (count < 0 || count > NF4DQ_GEMM_GROUP_MAX || (count > 0 && !mats)) return NF4DQ_ERR_ARG;
+    if (dtype != NF4DQ_F16 && dtype != NF4DQ_BF16) return NF4DQ_ERR_ARG;
+    if (M < 0 || K < 0) return NF4DQ_ERR_ARG;
+    int64_t ntot = 0;
+    for (int i = 0; i < count; ++i) {
+        const nf4_gemm_mat& m = mats[i];
+        if (m.N < 0 || m.nb <= 0 || m.n2 <= 0) return NF4DQ_ERR_ARG;
+        if (!m.packed || !m.absmax_q || !m.absmax2 || !m.y) return NF4DQ_ERR_ARG;
+        if (m.N % 64 || m.packed_len != m.N * (K / 2)) return NF4DQ_ERR_SHAPE;
+        ntot += m.N;
+    }
+    if (M == 0 || ntot == 0 || count == 0) return NF4DQ_OK;
+    if (!x) return NF4DQ_ERR_ARG;
+    if (M > NF4DQ_GEMM_MAX_M || K % kChunkK) return NF4DQ_ERR_SHAPE;
+    if ((size_t)(ntot / 16) * 4 > kCounterBytes) return NF4DQ_ERR_TOO_LARGE;
+    nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, ntot, K);
+    if (cfg.kernel == 0) cfg.kernel = default_gemm_cfg(M, ntot, K).kernel;
+    if (cfg.kernel != NF4DQ_GEMM_STREAM) {
+        for (int i = 0; i < count; ++i) {
+            const nf4_gemm_mat& m = mats[i];
+            const int rc = gemm_impl(x, M, m.packed, m.packed_len, m.absmax_q, m.nb, m.absmax2, m.n2, m.y, dtype, m.N,
+                                     K, workspace, workspace_bytes, cfgp, st);
+            if (rc) return rc;
+        }
+        return NF4DQ_OK;
+    }
+    for (int i = 0; i < count; ++i) {
+        if (mats[i].N == 0) return NF4DQ_ERR_SHAPE;  // an empty weight cannot own strip groups
+        if (!valid_gemm_cfg(cfg, M, mats[i].N, K)) return NF4DQ_ERR_ARG;
+        if (mats[i].packed_len >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
+    }
+    if (M * K * 2 >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
+    const size_t need = cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
+    if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
+    HostMat h[NF4DQ_GEMM_GROUP_MAX];
+    for (int i = 0; i < count; ++i)
+        h[i] = HostMat{mats[i].packed, mats[i].packed_len, mats[i].absmax_q, mats[i].nb, mats[i].absmax2,
+                       mats[i].n2, mats[i].y, mats[i].N};
+    return launch_stream(h, count, x, M, K, dtype, cfg, workspace, st);
+}
+
+static size_t grouped_workspace(int64_t M, int64_t K, const nf4_gemm_mat* mats, int32_t count,
+                                const nf4_gemm_cfg* cfgp) {
+    if (count <= 0 || !mats || M <= 0 || K <= 0 || K % kChunkK) return 0;
+    int64_t ntot = 0, nmax = 0;
+    for (int i = 0; i < count; ++i) {
+        ntot += mats[i].N;
+        nmax = mats[i].N > nmax ? mats[i].N : nmax;
+    }
+    if (ntot <= 0) return 0;
+    nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, ntot, K);
+    if (cfg.kernel == 0) cfg.kernel = default_gemm_cfg(M, ntot, K).kernel;
+    if (cfg.kernel == NF4DQ_GEMM_STREAM)
+        return cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
+    size_t w = 0;  // per-weight launches: the largest of their needs
+    for (int i = 0; i < count; ++i) {
+        const nf4_gemm_cfg c = cfgp ? *cfgp : default_gemm_cfg(M, mats[i].N, K);
+        const size_t wi = workspace_for(M, mats[i].N, K, c);
+        w = wi > w ? wi : w;
+    }
+    (void)nmax;
+    return w;
+}
+
 }  // namespace
 
 extern "C" {
@@ -790,6 +952,18 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
                  void* workspace, size_t workspace_bytes, void* hip_stream) {
     return gemm_impl(x, M, packed, packed_len, absmax_q, nb, absmax2, n2, y, dtype, N, K, workspace, workspace_bytes,
                      nullptr, reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+size_t nf4_gemm_grouped_workspace_bytes(int64_t M, int64_t K, const nf4_gemm_mat* mats, int32_t count,
+                                        const nf4_gemm_cfg* cfg) {
+    return grouped_workspace(M, K, mats, count, cfg);
+}
+
+int nf4_gemm_ref_grouped(const void* x, int64_t M, int64_t K, const nf4_gemm_mat* mats, int32_t count,
+                         int32_t out_dtype, void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfg,
+                         void* hip_stream) {
+    return gemm_grouped_impl(x, M, K, mats, count, out_dtype, workspace, workspace_bytes, cfg,
+                             reinterpret_cast<hipStream_t>(hip_stream));
 }
 
 int nf4_gemm_ref_cfg(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,

@@ -28,7 +28,7 @@ parity unpinned) and ``dequantize_nf4_into`` (caller-provided output).
 from __future__ import annotations
 
 import ctypes
-from typing import Iterable, List, Optional
+from typing import Iterable, List, Optional, Sequence
 
 import torch
 
@@ -303,3 +303,66 @@ def nf4_linear(x: torch.Tensor, module, bias: Optional[torch.Tensor] = None) -> 
     if bias is not None:
         y = y + bias.to(y.dtype)
     return y.reshape(*lead, N)
+
+
+def nf4_linear_grouped(x: torch.Tensor, modules: Sequence, biases: Optional[Sequence] = None) -> List[torch.Tensor]:
+    """``[x @ W_i.t() (+ b_i)]`` for NF4 weights W_i that share the input x (q/k/v, gate/up).
+
+    One fused launch for all of them (``nf4_gemm_ref_grouped``) when every
+    weight meets ``nf4_linear``'s fused-path rules, has the same ``in_features``
+    and output dtype, and there are at most ``GEMM_GROUP_MAX`` of them;
+    otherwise each goes through ``nf4_linear``.  Results are the same values
+    ``nf4_linear`` gives per weight (same dequantized weights, fp32
+    accumulation; the summation order may differ).
+    """
+    modules = list(modules)
+    biases = list(biases) if biases is not None else [None] * len(modules)
+    if len(biases) != len(modules):
+        raise ValueError("nf4_linear_grouped: one bias (or None) per module")
+    if not modules:
+        return []
+    preps = [_prepare(mod) for mod in modules]
+    K = x.shape[-1]
+    lead = x.shape[:-1]
+    M = x.numel() // K if K else 0
+    dtype = preps[0][3]
+    dev = preps[0][0].device
+    grouped = 1 < len(modules) <= _lib.GEMM_GROUP_MAX and 0 < M <= _lib.GEMM_MAX_M and K % 128 == 0
+    for (q, a1, _a2, dt, m, n) in preps:
+        grouped = grouped and (dt == dtype and dt in (torch.float16, torch.bfloat16) and n == K and m % 64 == 0
+                               and a1.dtype == torch.uint8 and q.dtype == torch.uint8 and q.device == dev
+                               and q.numel() == m * K // 2)
+    if not grouped:
+        return [nf4_linear(x, mod, bias=b) for mod, b in zip(modules, biases)]
+    _require_device(preps[0][0])
+    xc = x.reshape(M, K)
+    if xc.dtype != dtype:
+        xc = xc.to(dtype)
+    xc = xc.contiguous()
+    ys, keep = [], []
+    mats = (_lib.GemmMat * len(modules))()
+    for i, (q, a1, a2, _dt, m, _n) in enumerate(preps):
+        y = torch.empty((M, m), dtype=dtype, device=dev)
+        _, qp, qn = _flat_ptr(q)
+        _, ap, an = _flat_ptr(a1)
+        a2f = a2 if a2.dtype == torch.float32 else a2.to(torch.float32)
+        a2f, bp, bn = _flat_ptr(a2f)
+        if an == 0 or bn == 0:
+            raise ZeroDivisionError("integer division or modulo by zero (empty absmax)")
+        keep.append(a2f)
+        mats[i] = _lib.GemmMat(qp, qn, ap, an, bp, bn, y.data_ptr(), m)
+        ys.append(y)
+    L = _lib.lib()
+    with torch.cuda.device(dev):
+        ws_bytes = L.nf4_gemm_grouped_workspace_bytes(M, K, mats, len(modules), None)
+        ws = _gemm_workspace(dev, ws_bytes) if ws_bytes else None
+        rc = L.nf4_gemm_ref_grouped(xc.data_ptr(), M, K, mats, len(modules), _dtype_code(dtype),
+                                    ws.data_ptr() if ws is not None else None, ws_bytes, None,
+                                    torch.cuda.current_stream().cuda_stream)
+    _lib.check(rc, "nf4 fused grouped gemm")
+    out = []
+    for y, b, (_q, _a1, _a2, _dt, m, _n) in zip(ys, biases, preps):
+        if b is not None:
+            y = y + b.to(y.dtype)
+        out.append(y.reshape(*lead, m))
+    return out

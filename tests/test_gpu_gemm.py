@@ -199,3 +199,57 @@ def test_invalid_decompositions_rejected(gpu):
     c = _lib.GemmCfg(_lib.GEMM_STREAM, 8, 4, 1, 1)
     assert L.nf4_gemm_ref_cfg(F, 1, F, 64 * 64, F, 128, F, 1, F, _lib.BF16, 64, 128, F, 1 << 30,
                               ctypes.byref(c), None) == _lib.ERR_ARG
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,K,Ns", [(1, 4096, (4096, 1024, 1024)), (4, 2048, (512, 1536)),
+                                    (3, 1280, (64, 128, 192, 256, 320, 384, 448, 512)), (16, 512, (1024, 64))])
+def test_grouped_gemm_vs_float64_oracle(coracle, gpu, dt, M, K, Ns):
+    """Weights sharing x in one launch: each output against its own float64 oracle."""
+    from nf4_triton_dequantization_amd import nf4_linear_grouped
+
+    mods, Ws = [], []
+    for i, N in enumerate(Ns):
+        packed, a1, a2 = O.make_inputs(N, K, seed=N + K + 11 * i, a2_kind="normal")
+        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16))
+        mods.append(make_module(packed, a1, a2, N, K, dt, gpu))
+    xt, xb = _x_bits(M, K, dt, seed=M + 3)
+    ys = nf4_linear_grouped(xt.to(gpu), mods)
+    assert len(ys) == len(Ns)
+    for y, W, N in zip(ys, Ws, Ns):
+        assert y.shape == (M, N)
+        _check(y, xb, W, dt)
+
+
+def test_grouped_gemm_split_k_and_wrapping(coracle, gpu):
+    """Grouped launch with a K split across workgroups and absmax that wraps (reference repeat)."""
+    import ctypes
+
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    M, K = 2, 1024
+    Ns = (256, 128)
+    specs = [(O.golden_case_inputs(256, K, 5, {"nb": 37, "n2": 5})[:3]), O.make_inputs(128, K, seed=9)]
+    mats = (_lib.GemmMat * 2)()
+    ys, keep, Ws = [], [], []
+    for i, ((packed, a1, a2), N) in enumerate(zip(specs, Ns)):
+        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16))
+        t = [torch.from_numpy(v).to(gpu) for v in (packed, a1, a2)]
+        keep.append(t)
+        y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+        ys.append(y)
+        mats[i] = _lib.GemmMat(t[0].data_ptr(), t[0].numel(), t[1].data_ptr(), t[1].numel(), t[2].data_ptr(),
+                               t[2].numel(), y.data_ptr(), N)
+    xt, xb = _x_bits(M, K, "bf16", seed=21)
+    x = xt.to(gpu)
+    for ks in (1, 2, 3):
+        cfg = _lib.GemmCfg(_lib.GEMM_STREAM, 8, 2, ks, 2)
+        wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, mats, 2, ctypes.byref(cfg))
+        ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=gpu)
+        rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, mats, 2, _lib.BF16, ws.data_ptr(), wsz, ctypes.byref(cfg),
+                                    torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+        for y, W in zip(ys, Ws):
+            _check(y, xb, W, "bf16")
