@@ -300,7 +300,8 @@ struct SSlot {
 // Diagnostic builds only (tools/Makefile): 1 = loads without the dequant/MMA
 // body, 2 = the body on register-made data without weight loads, 3 = per-wave
 // s_memrealtime stamps (start, prologue done, loop done, end) into the
-// workspace after the counter region (ksplit 1 only).
+// workspace after the counter region (ksplit 1 only), 4 = no absmax loads,
+// 5 = neither weight loads nor dequant, 6 = no activation loads (x staged from registers).
 #ifndef NF4_STREAM_DEBUG
 #define NF4_STREAM_DEBUG 0
 #endif
@@ -451,25 +452,32 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
         const uint32_t p = tid + (uint32_t)i * 64u * W;
         const uint32_t r = fdiv(p, A.ppr), q = p - r * A.ppr.d;
         const bool ok = p < pieces && s0 * 256u + q * 8u < A.K;
+#if NF4_STREAM_DEBUG == 6
+        xv[i] = u32x4{p, r, q, (uint32_t)ok};
+        (void)rx;
+#else
         xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? (r * A.K + s0 * 256u) * 2u + q * 16u : kOob, 0, 0);
+#endif
         xdst[i] = p < pieces ? kLdsX + r * A.xstride + q * 16u : 0xFFFFFFFFu;
     }
     // 2. the weight ring (VS: the wave's scales first)
     // (issue order = the loop's: slot by slot, w0 w1 qa qb -- the scheduler must
     // not regroup them, or the waitcnt pass merges two orders into a drain)
-    constexpr int NV = VS ? kVsMax / 4 : 1;
-    u32x4 a1v[NV], a2v[NV];
+    // VS: scales of 4 chunks per 16-byte pair of loads, two groups live (the
+    // next group's pair is issued as the current one starts)
+    u32x4 a1v[2], a2v[2];
+    uint32_t b1 = 0, b2 = 0;
+    auto scale_issue = [&](int g) {
+        const uint32_t oob = 4u * g < cnt ? 0u : kOob;  // groups past the wave's range: no traffic
+        a1v[g & 1] = __builtin_amdgcn_raw_buffer_load_b128(ra1, (b1 + 16u * g) | oob, 0, 0);
+        a2v[g & 1] = __builtin_amdgcn_raw_buffer_load_b128(ra2, ((b2 + 4u * g) * 4u) | oob, 0, 0);
+    };
     if constexpr (VS) {
         const uint32_t cf = s0 + l0;
         // the row's wrapped bases (reference repeat semantics, :173-186); no wrap inside the row
-        const uint32_t b1 = fmodu(row * A.bpr, Mt.nb) + 4u * cf;
-        const uint32_t b2 = fmodu(row * A.groups, Mt.n2) + cf;
-#pragma unroll
-        for (int g = 0; g < NV; ++g) {
-            const uint32_t oob = 4u * g < cnt ? 0u : kOob;  // groups past the wave's range: no traffic
-            a1v[g] = __builtin_amdgcn_raw_buffer_load_b128(ra1, (b1 + 16u * g) | oob, 0, 0);
-            a2v[g] = __builtin_amdgcn_raw_buffer_load_b128(ra2, ((b2 + 4u * g) * 4u) | oob, 0, 0);
-        }
+        b1 = fmodu(row * A.bpr, Mt.nb) + 4u * cf;
+        b2 = fmodu(row * A.groups, Mt.n2) + cf;
+        scale_issue(0);
         __builtin_amdgcn_sched_barrier(0);
     }
     SSlot ring[P];
@@ -526,9 +534,13 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
 #pragma unroll
         for (int jj = 0; jj < kVsMax; ++jj) {
             const int j = jj % P;
+            if (jj % 4 == 0 && jj + 4 < kVsMax) {
+                scale_issue(jj / 4 + 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             if ((uint32_t)jj < cnt)  // uniform
-                body((uint32_t)jj, j, (a1v[jj / 4][jj % 4] >> (8u * kh)) & 0xFFu,
-                     __uint_as_float(a2v[jj / 4][jj % 4]));
+                body((uint32_t)jj, j, (a1v[(jj / 4) & 1][jj % 4] >> (8u * kh)) & 0xFFu,
+                     __uint_as_float(a2v[(jj / 4) & 1][jj % 4]));
             __builtin_amdgcn_sched_barrier(0);
             // unconditional (past the range: out-of-range offsets, no traffic), so
             // both sides of the guard leave the same loads pending

@@ -7,6 +7,8 @@
 //   1  coalesced: instruction i, lane l loads row 8 i + (l >> 3), 16 B piece l & 7
 //      (each 16-lane group reads two whole lines)
 //   2  prepacked: the chunk's 2 KiB are contiguous, instruction i lane l at i*1024 + 16 l
+//   3  pattern 0 with contiguous chunk ranges per part (part p: chunks [p cnt, p cnt + cnt))
+//   4  pattern 3 with the range walked from a per-strip rotation (strip mod cnt)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -23,6 +25,29 @@ __global__ __launch_bounds__(256) void lp_kernel(const uint8_t* w, uint32_t rows
     const uint32_t parts = strips_per_wave_group;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, rows * row_bytes, 0x00020000);
     uint32_t acc = 0;
+    const uint32_t cnt = (chunks + parts - 1) / parts;
+    if constexpr (PAT >= 3) {
+        const uint32_t rot = PAT == 4 ? strip % cnt : 0u;
+        for (uint32_t j0 = 0; j0 < cnt; j0 += P) {
+            u32x4 v[P][2];
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const uint32_t j = j0 + p;
+                const uint32_t jr = j + rot < cnt ? j + rot : j + rot - cnt;
+                const uint32_t c = part * cnt + jr;
+                const bool ok = j < cnt && c < chunks;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const uint32_t off = (strip * 16u + (lane & 15u)) * row_bytes + c * 128u + (lane >> 4) * 32u + 16u * i;
+                    v[p][i] = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? off : 0x80000000u, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < P; ++p) acc ^= v[p][0].x ^ v[p][0].w ^ v[p][1].y ^ v[p][1].z;
+        }
+        if (acc == 0x12345678u) out[0] = acc;
+        return;
+    }
     for (uint32_t c0 = part; c0 < chunks; c0 += parts * P) {
         u32x4 v[P][2];
 #pragma unroll
@@ -55,9 +80,9 @@ extern "C" int lp_launch(int pat, int depth, const void* w, uint32_t rows, uint3
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define L_(PA, PP) hipLaunchKernelGGL((lp_kernel<PA, PP>), grid, block, 0, st, (const uint8_t*)w, rows, row_bytes, parts, (uint32_t*)out)
     if (depth == 2) {
-        if (pat == 0) L_(0, 2); else if (pat == 1) L_(1, 2); else L_(2, 2);
+        if (pat == 0) L_(0, 2); else if (pat == 1) L_(1, 2); else if (pat == 2) L_(2, 2); else if (pat == 3) L_(3, 2); else L_(4, 2);
     } else {
-        if (pat == 0) L_(0, 4); else if (pat == 1) L_(1, 4); else L_(2, 4);
+        if (pat == 0) L_(0, 4); else if (pat == 1) L_(1, 4); else if (pat == 2) L_(2, 4); else if (pat == 3) L_(3, 4); else L_(4, 4);
     }
 #undef L_
     return (int)hipGetLastError();
