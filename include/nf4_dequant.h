@@ -149,9 +149,13 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
  * wave 2/4/8 (8 not with 16 waves; 16 waves only when M <= 16), strips = 16-column strips per workgroup
  * 1/2/4 dividing waves) or NF4DQ_GEMM_K128 (waves 4/8, depth 1/2/4 (<= 2 when
  * M > 16), strips ignored).  ksplit: K slices reduced across workgroups.
+ * NF4DQ_GEMM_PERSIST: the streaming kernel's persistent form (M <= 16,
+ * ksplit 1, waves / strips K parts dividing K / 256 into a multiple of depth
+ * (2/4), x[M][K] in LDS, absmax not wrapping inside a row).
  * An invalid combination returns NF4DQ_ERR_ARG. */
 #define NF4DQ_GEMM_K128 1
 #define NF4DQ_GEMM_STREAM 2
+#define NF4DQ_GEMM_PERSIST 3
 typedef struct nf4_gemm_cfg {
     int32_t kernel;
     int32_t waves;

@@ -61,6 +61,7 @@ class LaunchCfg(ctypes.Structure):
 CFG_NT_LOADS = 1
 GEMM_K128 = 1
 GEMM_STREAM = 2
+GEMM_PERSIST = 3
 
 
 GEMM_GROUP_MAX = 8

@@ -272,7 +272,8 @@ struct StreamArgs {
     FastDiv ppr;            // 16-byte x pieces per staged row (cps * 32)
     uint32_t xstride;       // LDS bytes per staged x row
     uint32_t zero_off;      // 128 zero bytes: the A operand of rows >= M
-    uint32_t red_off;       // [W][MT][64] f32x4 partial sums
+    uint32_t red_off;       // [W][MT][64] f32x4 partial sums (persistent: two sets)
+    uint32_t out_off;       // persistent: finished outputs [group][strip][M][16] (16-bit)
     unsigned long long* stamps;  // NF4_STREAM_DEBUG == 3 only
 };
 
@@ -622,6 +623,181 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Persistent form of the streaming kernel (M <= 16, whole-K activation rows in
+// LDS, absmax without in-row wrap).  One workgroup per CU walks strip groups
+// (of every weight of a grouped launch) with a grid stride; each wave's ring
+// runs on ACROSS groups, so a launch pays the first-data latency, the LDS
+// tables and the activation staging once per CU instead of once per
+// workgroup.  The ring advances a round (P chunks) at a time; the absmax bytes
+// and nested scales of a round come in two loads issued ahead of its weights.
+// Finished groups are combined in LDS (double-buffered, one barrier per group)
+// and held there until the end, so that no global store sits between the
+// ring's loads (a store would turn every counted wait into a drain).
+template <int P>
+struct PScales {
+    typedef uint32_t vec __attribute__((ext_vector_type(P)));
+    vec a1, a2;
+};
+
+template <int P>
+__device__ __forceinline__ typename PScales<P>::vec pload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    if constexpr (P == 2) return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    else return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+
+struct PGeo {  // where the ring issues: one strip of one weight
+    __amdgpu_buffer_rsrc_t rw, ra1, ra2;
+    uint32_t row, b1, b2;
+};
+
+template <int DT, int W, int P>
+__global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ __attribute__((aligned(16))) f32x2 ptab[256 * 32];
+    __shared__ float qtab[256];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t nl = lane & 15u, kh = lane >> 4;
+    const uint32_t strip_in = wave % A.T, part = wave / A.T;
+    const uint32_t G = gridDim.x;
+    const uint32_t mine = A.sg_total > blockIdx.x ? (A.sg_total - blockIdx.x + G - 1u) / G : 0u;
+    const uint32_t cnt = A.cpp;  // chunks per wave per group (host: parts * cnt == chunks, cnt % P == 0)
+    const uint32_t rounds = cnt / P, total = mine * rounds;
+    const uint32_t l0 = part * cnt;
+
+    auto geo = [&](uint32_t it, PGeo& g) {
+        const uint32_t sgi = blockIdx.x + it * G;
+        uint32_t mi = 0;
+        for (uint32_t i = 1; i < A.nmat; ++i) mi = sgi >= A.mat[i].sg_begin ? i : mi;
+        const StreamMat& Mt = A.mat[mi];
+        g.row = ((sgi - Mt.sg_begin) * A.T + strip_in) * 16u + nl;
+        g.rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);
+        g.ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a1, 0, Mt.nb_bytes, kRsrcFlags);
+        g.ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a2, 0, Mt.n2_bytes, kRsrcFlags);
+        g.b1 = fmodu(g.row * A.bpr, Mt.nb) + 4u * l0;   // reference wrap (:173-186), none inside a row
+        g.b2 = fmodu(g.row * A.groups, Mt.n2) + l0;
+    };
+    // issue pointer: group it2, round rr2 of it
+    PGeo gi;
+    uint32_t it2 = 0, rr2 = 0;
+    geo(0, gi);
+    auto issue_scales = [&](PScales<P>& sc, bool valid) {
+        const uint32_t oob = valid ? 0u : kOob;
+        sc.a1 = pload<P>(gi.ra1, (gi.b1 + 4u * P * rr2) | oob);
+        sc.a2 = pload<P>(gi.ra2, ((gi.b2 + P * rr2) * 4u) | oob);
+    };
+    auto issue_w = [&](SSlot& sl, int s, bool valid) {
+        const uint32_t c = l0 + rr2 * P + (uint32_t)s;
+        const uint32_t woff = (gi.row * (A.K >> 1) + c * 128u + kh * 32u) | (valid ? 0u : kOob);
+        sl.w0 = __builtin_amdgcn_raw_buffer_load_b128(gi.rw, woff, 0, 0);
+        sl.w1 = __builtin_amdgcn_raw_buffer_load_b128(gi.rw, woff + 16u, 0, 0);
+    };
+    auto advance = [&]() {  // uniform
+        if (++rr2 == rounds) {
+            rr2 = 0;
+            ++it2;
+            if (it2 < mine) geo(it2, gi);
+        }
+    };
+
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
+    // 1. x rows (whole K), then round 0 of the ring
+    const uint32_t pieces = A.M * A.ppr.d;
+    u32x4 xv[kXR];
+    uint32_t xdst[kXR];
+#pragma unroll
+    for (int i = 0; i < kXR; ++i) {
+        const uint32_t p = tid + (uint32_t)i * 64u * W;
+        const uint32_t r = fdiv(p, A.ppr), q = p - r * A.ppr.d;
+        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, p < pieces ? r * A.K * 2u + q * 16u : kOob, 0, 0);
+        xdst[i] = p < pieces ? kLdsX + r * A.xstride + q * 16u : 0xFFFFFFFFu;
+    }
+    PScales<P> sc[2];
+    SSlot ring[P];
+    issue_scales(sc[0], total > 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+        issue_w(ring[s], s, total > 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    advance();
+    // 2. tables while the loads fly, then the x rows, one barrier
+    if (tid < 256u) qtab[tid] = (float)tid / 127.0f;
+    if (tid < 8u) *reinterpret_cast<u32x4*>(smem + A.zero_off + 16u * tid) = u32x4{0u, 0u, 0u, 0u};
+    for (uint32_t u = tid; u < 16u * 32u; u += 64u * W) {
+        const float clo = nf4_code(u >> 5);
+#pragma unroll
+        for (int hi = 0; hi < 16; ++hi) ptab[(16u * hi + (u >> 5)) * 32u + (u & 31u)] = f32x2{nf4_code(hi), clo};
+    }
+#pragma unroll
+    for (int i = 0; i < kXR; ++i)
+        if (xdst[i] != 0xFFFFFFFFu) *reinterpret_cast<u32x4*>(smem + xdst[i]) = xv[i];
+    __syncthreads();
+
+    const bool live = nl < A.M;
+    const uint32_t xa0 = live ? kLdsX + nl * A.xstride + kh * 128u : A.zero_off;
+    const uint32_t slot8 = (lane & 31u) * 8u;
+    f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+    uint32_t it = 0, rr = 0, buf = 0;
+
+    auto round = [&](PScales<P>& cur, PScales<P>& nxt) {
+        const bool more = it2 < mine;  // the issue pointer is one round ahead
+        issue_scales(nxt, more);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            const uint32_t l = l0 + rr * P + (uint32_t)s;
+            const uint32_t xa[1] = {live ? xa0 + l * 512u : xa0};
+            sslot_mma<DT, 1>(ring[s], (cur.a1[s] >> (8u * kh)) & 0xFFu, __uint_as_float(cur.a2[s]), ptab, qtab, smem,
+                             slot8, xa, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            issue_w(ring[s], s, more);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        advance();
+        if (++rr == rounds) {  // group `it` done (uniform)
+            f32x4* red = reinterpret_cast<f32x4*>(smem + A.red_off) + buf * (64u * W);
+            red[wave * 64u + lane] = acc[0];
+            __syncthreads();
+            if (part == 0) {
+                f32x4 sum = red[wave * 64u + lane];
+                for (uint32_t q = 1; q < A.parts; ++q) sum += red[(wave + q * A.T) * 64u + lane];
+                uint16_t* o = reinterpret_cast<uint16_t*>(smem + A.out_off) + ((it * A.T + strip_in) * A.M) * 16u;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t m = 4u * kh + r;
+                    if (m < A.M) o[m * 16u + nl] = (uint16_t)(pack2<DT>(sum[r], 0.0f) & 0xFFFFu);
+                }
+            }
+            acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+            buf ^= 1u;
+            rr = 0;
+            ++it;
+        }
+    };
+    for (uint32_t g = 0; g < total; g += 2) {
+        round(sc[0], sc[1]);
+        if (g + 1 < total) round(sc[1], sc[0]);
+    }
+    // 3. the workgroup's outputs
+    __syncthreads();
+    const uint16_t* o = reinterpret_cast<const uint16_t*>(smem + A.out_off);
+    const uint32_t per = A.T * A.M * 16u;
+    for (uint32_t i = tid; i < mine * per; i += 64u * W) {
+        const uint32_t ito = i / per, rem = i - ito * per;
+        const uint32_t t = rem / (A.M * 16u), rem2 = rem - t * (A.M * 16u);
+        const uint32_t sgi = blockIdx.x + ito * G;
+        uint32_t mi = 0;
+        for (uint32_t j = 1; j < A.nmat; ++j) mi = sgi >= A.mat[j].sg_begin ? j : mi;
+        const StreamMat& Mt = A.mat[mi];
+        const uint32_t col = ((sgi - Mt.sg_begin) * A.T + t) * 16u + (rem2 & 15u);
+        reinterpret_cast<uint16_t*>(Mt.y)[(rem2 >> 4) * Mt.N + col] = o[i];
+    }
+}
+
 // ---- decomposition choice --------------------------------------------------
 constexpr uint32_t kLdsPerCu = 160 * 1024;
 constexpr uint32_t kStreamStatic = 256 * 32 * 8 + 1024;  // pair table, q/127 table
@@ -654,20 +830,52 @@ static bool stream_fits(int64_t M, int64_t K, const nf4_gemm_cfg& c) {
 // the streaming kernel for decode-sized M (8 waves, 2 chunks in flight, whole K
 // per workgroup; 4 strips per workgroup for wide N; a 2-way K split for long K
 // once M > 1), the 128-deep kernel for 16 < M and for narrow N at M = 16.
+bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K);
+
 nf4_gemm_cfg default_gemm_cfg(int64_t M, int64_t N, int64_t K) {
+    // N = all columns of the launch (a grouped launch passes the sum)
     if (K % kSChunkK == 0 && (M <= 8 || (M <= 16 && N >= 8192))) {
-        nf4_gemm_cfg c{NF4DQ_GEMM_STREAM, 8, 2, 1, N >= 8192 ? 4 : 1};
-        if (M > 8) c.ksplit = 2;
-        else if (M > 1 && K >= 8192) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 2, 2};
+        nf4_gemm_cfg c{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};
+        if (M > 8) {
+            c.ksplit = 2;
+            c.strips = 4;
+        } else if (K >= 8192) {
+            if (M > 1) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 2, 2};
+        } else if (N >= 16384) {
+            c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 4, 2, 1, 4};
+        } else if (N >= 8192) {
+            c.strips = 4;
+        } else if (N > 4096) {  // q/k/v-sized launches: persistent form (falls back if absmax wraps in a row)
+            c = nf4_gemm_cfg{NF4DQ_GEMM_PERSIST, 8, 2, 1, 2};
+        } else if (K == 4096) {
+            c.kernel = NF4DQ_GEMM_PERSIST;
+        }
+        if (c.kernel == NF4DQ_GEMM_PERSIST && !valid_gemm_cfg(c, M, N, K)) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};
         while (c.ksplit < K / kSChunkK && !stream_fits(M, K, c)) ++c.ksplit;
-        if (N % (16 * c.strips)) c.strips = 1;
         return c;
     }
     nf4_gemm_cfg c{NF4DQ_GEMM_K128, 8, M > 16 ? 1 : 2, 1, 1};
     return c;
 }
 
+static uint32_t persist_dyn_bytes(int64_t M, int64_t K, const nf4_gemm_cfg& c, uint32_t groups_per_wg) {
+    const uint32_t xstride = (uint32_t)K * 2u + 16u;
+    const uint32_t out = (groups_per_wg * (uint32_t)c.strips * (uint32_t)M * 32u + 15u) & ~15u;
+    return kLdsX + (uint32_t)M * xstride + 128u + 2u * (uint32_t)c.waves * 1024u + out;
+}
+
 bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
+    if (c.kernel == NF4DQ_GEMM_PERSIST) {
+        if (K % kSChunkK || M > 16) return false;
+        if (c.waves != 4 && c.waves != 8 && c.waves != 16) return false;
+        if (c.depth != 2 && c.depth != 4) return false;
+        if (c.strips != 1 && c.strips != 2 && c.strips != 4) return false;
+        if (c.waves % c.strips || N % (16 * c.strips) || c.ksplit != 1) return false;
+        const int64_t chunks = K / kSChunkK, parts = c.waves / c.strips;
+        if (chunks % parts || (chunks / parts) % c.depth) return false;
+        if (M * (K / 8) > (int64_t)kXR * 64 * c.waves) return false;
+        return persist_dyn_bytes(M, K, c, 1) + kStreamStatic <= kLdsPerCu;
+    }
     if (c.kernel == NF4DQ_GEMM_STREAM) {
         if (K % kSChunkK) return false;
         if (c.waves != 4 && c.waves != 8 && c.waves != 16) return false;
@@ -697,6 +905,18 @@ static size_t counters_bytes(int64_t) { return kCounterBytes; }
 static size_t workspace_for(int64_t M, int64_t N, int64_t K, const nf4_gemm_cfg& c) {
     if (M <= 0 || N <= 0 || K <= 0 || N % 64 || K % kChunkK) return 0;
     return c.ksplit > 1 ? counters_bytes(N) + (size_t)c.ksplit * (size_t)M * (size_t)N * sizeof(float) : 0;
+}
+
+static int device_cus() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cached[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return cached[dev];
 }
 
 struct HostMat {
@@ -807,6 +1027,91 @@ static int launch_stream(const HostMat* mats, int count, const void* x, int64_t 
     return hip_rc2(hipGetLastError());
 }
 
+// One launch of the persistent kernel over `count` weights sharing x (cfg
+// validated per weight).  Grid: as many workgroups as fit the CUs at once.
+static int launch_persist(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
+                          const nf4_gemm_cfg& cfg, hipStream_t st) {
+    StreamArgs S{};
+    S.nmat = (uint32_t)count;
+    S.x = x;
+    S.M = (uint32_t)M;
+    S.K = (uint32_t)K;
+    S.T = (uint32_t)cfg.strips;
+    S.parts = (uint32_t)(cfg.waves / cfg.strips);
+    S.ksplit = 1;
+    S.chunks = (uint32_t)(K / kSChunkK);
+    S.cps = S.chunks;
+    S.cpp = S.chunks / S.parts;
+    S.bpr = (uint32_t)(K / 64);
+    S.groups = (S.bpr + 3) / 4;
+    S.ppr = make_fastdiv((uint32_t)(K / 8));
+    S.xstride = (uint32_t)K * 2u + 16u;
+    uint32_t sg = 0, strips = 0;
+    for (int i = 0; i < count; ++i) {
+        const HostMat& h = mats[i];
+        if (!(h.nb % (K / 64) == 0 || h.nb >= h.N * (K / 64)) ||
+            !(h.n2 % (int64_t)S.groups == 0 || h.n2 >= h.N * (int64_t)S.groups))
+            return NF4DQ_ERR_ARG;  // absmax wrapping inside a row: the streaming kernel's case
+        StreamMat& m = S.mat[i];
+        m.packed = h.packed;
+        m.a1 = h.a1;
+        m.a2 = h.a2;
+        m.y = h.y;
+        m.N = (uint32_t)h.N;
+        m.sg_begin = sg;
+        m.strip_begin = strips;
+        const int64_t nbc = h.nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : h.nb;
+        const int64_t n2c = h.n2 > (int64_t(1) << 29) ? (int64_t(1) << 29) : h.n2;
+        m.nb = make_fastdiv((uint32_t)nbc);
+        m.n2 = make_fastdiv((uint32_t)n2c);
+        m.nb_bytes = (uint32_t)nbc;
+        m.n2_bytes = (uint32_t)(n2c * 4);
+        sg += (uint32_t)(h.N / (16 * cfg.strips));
+        strips += (uint32_t)(h.N / 16);
+    }
+    S.sg_total = sg;
+    S.ncols = strips * 16u;
+    const uint32_t base = persist_dyn_bytes(M, K, cfg, 1) + kStreamStatic;
+    const uint32_t per_cu = kLdsPerCu / base > 0 ? kLdsPerCu / base : 1u;
+    uint32_t G = (uint32_t)device_cus() * per_cu;
+    if (G > sg) G = sg;
+    const uint32_t per_wg = (sg + G - 1) / G;
+    const uint32_t dyn = persist_dyn_bytes(M, K, cfg, per_wg);
+    if (dyn + kStreamStatic > kLdsPerCu) return NF4DQ_ERR_TOO_LARGE;
+    S.zero_off = kLdsX + (uint32_t)M * S.xstride;
+    S.red_off = S.zero_off + 128u;
+    S.out_off = S.red_off + 2u * (uint32_t)cfg.waves * 1024u;
+    const dim3 grid(G), block(64 * cfg.waves);
+#define NF4_PK(DT_, W_, P_)                                                                                    \
+    do {                                                                                                       \
+        static bool attr_ = false;                                                                             \
+        if (!attr_) {                                                                                          \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_persist_kernel<DT_, W_, P_>),    \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsCap);         \
+            attr_ = true;                                                                                      \
+        }                                                                                                      \
+        hipLaunchKernelGGL((nf4_gemm_persist_kernel<DT_, W_, P_>), grid, block, dyn, st, S);                  \
+    } while (0)
+#define NF4_PW(DT_)                                            \
+    do {                                                       \
+        if (cfg.waves == 4) {                                  \
+            if (cfg.depth == 2) NF4_PK(DT_, 4, 2);             \
+            else NF4_PK(DT_, 4, 4);                            \
+        } else if (cfg.waves == 8) {                           \
+            if (cfg.depth == 2) NF4_PK(DT_, 8, 2);             \
+            else NF4_PK(DT_, 8, 4);                            \
+        } else {                                               \
+            if (cfg.depth == 2) NF4_PK(DT_, 16, 2);            \
+            else NF4_PK(DT_, 16, 4);                           \
+        }                                                      \
+    } while (0)
+    if (dtype == NF4DQ_BF16) NF4_PW(NF4DQ_BF16);
+    else NF4_PW(NF4DQ_F16);
+#undef NF4_PW
+#undef NF4_PK
+    return hip_rc2(hipGetLastError());
+}
+
 static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,
                      int64_t nb, const float* absmax2, int64_t n2, void* y, int32_t dtype, int64_t N, int64_t K,
                      void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfgp, hipStream_t st) {
@@ -826,8 +1131,14 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     const uint32_t ks = (uint32_t)cfg.ksplit;
     const size_t need = workspace_for(M, N, K, cfg);
     if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
-    if (cfg.kernel == NF4DQ_GEMM_STREAM) {
+    if (cfg.kernel == NF4DQ_GEMM_STREAM || cfg.kernel == NF4DQ_GEMM_PERSIST) {
         const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
+        if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
+            const int rc = launch_persist(&h, 1, x, M, K, dtype, cfg, st);
+            if (rc != NF4DQ_ERR_ARG || cfgp) return rc;
+            cfg = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};  // library choice, absmax wrapping in a row
+            if (!valid_gemm_cfg(cfg, M, N, K)) return NF4DQ_ERR_ARG;
+        }
         return launch_stream(&h, 1, x, M, K, dtype, cfg, workspace, st);
     }
     GemmArgs A{};
@@ -898,7 +1209,7 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
     if ((size_t)(ntot / 16) * 4 > kCounterBytes) return NF4DQ_ERR_TOO_LARGE;
     nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, ntot, K);
     if (cfg.kernel == 0) cfg.kernel = default_gemm_cfg(M, ntot, K).kernel;
-    if (cfg.kernel != NF4DQ_GEMM_STREAM) {
+    if (cfg.kernel != NF4DQ_GEMM_STREAM && cfg.kernel != NF4DQ_GEMM_PERSIST) {
         for (int i = 0; i < count; ++i) {
             const nf4_gemm_mat& m = mats[i];
             const int rc = gemm_impl(x, M, m.packed, m.packed_len, m.absmax_q, m.nb, m.absmax2, m.n2, m.y, dtype, m.N,
@@ -919,6 +1230,13 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
     for (int i = 0; i < count; ++i)
         h[i] = HostMat{mats[i].packed, mats[i].packed_len, mats[i].absmax_q, mats[i].nb, mats[i].absmax2,
                        mats[i].n2, mats[i].y, mats[i].N};
+    if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
+        const int rc = launch_persist(h, count, x, M, K, dtype, cfg, st);
+        if (rc != NF4DQ_ERR_ARG || cfgp) return rc;
+        cfg = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};  // library choice, absmax wrapping in a row
+        for (int i = 0; i < count; ++i)
+            if (!valid_gemm_cfg(cfg, M, mats[i].N, K)) return NF4DQ_ERR_ARG;
+    }
     return launch_stream(h, count, x, M, K, dtype, cfg, workspace, st);
 }
 
@@ -933,7 +1251,7 @@ static size_t grouped_workspace(int64_t M, int64_t K, const nf4_gemm_mat* mats, 
     if (ntot <= 0) return 0;
     nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, ntot, K);
     if (cfg.kernel == 0) cfg.kernel = default_gemm_cfg(M, ntot, K).kernel;
-    if (cfg.kernel == NF4DQ_GEMM_STREAM)
+    if (cfg.kernel == NF4DQ_GEMM_STREAM || cfg.kernel == NF4DQ_GEMM_PERSIST)
         return cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
     size_t w = 0;  // per-weight launches: the largest of their needs
     for (int i = 0; i < count; ++i) {

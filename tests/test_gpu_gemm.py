@@ -165,7 +165,7 @@ def test_every_decomposition_agrees_with_oracle(coracle, gpu, dt, M, N, K):
     tol = torch.from_numpy(2.0 ** -p * np.abs(xf @ wf.T) + 2.0 ** -20 * (np.abs(xf) @ np.abs(wf).T)).to(gpu)
     y = torch.empty((M, N), dtype=x.dtype, device=gpu)
     ran = 0
-    for kernel in (_lib.GEMM_STREAM, _lib.GEMM_K128):
+    for kernel in (_lib.GEMM_PERSIST, _lib.GEMM_STREAM, _lib.GEMM_K128):
         for waves in (4, 8, 16):
             for depth in (1, 2, 4, 8):
                 for strips in ((1, 2, 4) if kernel != _lib.GEMM_K128 else (1,)):
@@ -253,3 +253,36 @@ def test_grouped_gemm_split_k_and_wrapping(coracle, gpu):
         torch.cuda.synchronize()
         for y, W in zip(ys, Ws):
             _check(y, xb, W, "bf16")
+
+
+@pytest.mark.parametrize("cfg", [(8, 2, 1), (4, 2, 2), (8, 4, 2), (16, 2, 2), (4, 4, 4)])
+def test_persistent_grouped_gemm(coracle, gpu, cfg):
+    """The persistent kernel over a grouped launch (several weights, several strip groups per workgroup)."""
+    import ctypes
+
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    waves, depth, strips = cfg
+    M, K = 3, 4096  # 16 chunks: every cfg above splits them into a multiple of its depth
+    Ns = (4096, 1024, 2048)
+    mats = (_lib.GemmMat * len(Ns))()
+    ys, keep, Ws = [], [], []
+    for i, N in enumerate(Ns):
+        packed, a1, a2 = O.make_inputs(N, K, seed=7 * N + i, a2_kind="normal")
+        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16))
+        t = [torch.from_numpy(v).to(gpu) for v in (packed, a1, a2)]
+        keep.append(t)
+        y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+        ys.append(y)
+        mats[i] = _lib.GemmMat(t[0].data_ptr(), t[0].numel(), t[1].data_ptr(), t[1].numel(), t[2].data_ptr(),
+                               t[2].numel(), y.data_ptr(), N)
+    xt, xb = _x_bits(M, K, "bf16", seed=4)
+    x = xt.to(gpu)
+    c = _lib.GemmCfg(_lib.GEMM_PERSIST, waves, depth, 1, strips)
+    rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, mats, len(Ns), _lib.BF16, None, 0, ctypes.byref(c),
+                                torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    for y, W in zip(ys, Ws):
+        _check(y, xb, W, "bf16")

@@ -68,6 +68,10 @@ def main():
             res = []
             cfgs = []
             for waves in (4, 8, 16):
+                for depth in (2, 4):
+                    for strips in (1, 2, 4):
+                        cfgs.append(_lib.GemmCfg(_lib.GEMM_PERSIST, waves, depth, 1, strips))
+            for waves in (4, 8, 16):
                 for depth in (2, 4, 8):
                     for strips in (1, 2, 4):
                         for ks in (1, 2, 4):
