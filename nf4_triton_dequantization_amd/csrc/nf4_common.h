@@ -43,13 +43,17 @@ __device__ __forceinline__ float opaque(float x) {
     return x;
 }
 
+// The pair as one opaque 64-bit value (non-volatile: the scheduler may still
+// move it; the products stay one v_pk_mul_f32).
+__device__ __forceinline__ f32x2 opaque2(f32x2 v) {
+    asm("" : "+v"(v));
+    return v;
+}
+
 template <int DT>
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-    if constexpr (DT == NF4DQ_F16) {
-        lo = opaque(lo);
-        hi = opaque(hi);
-    }
     f32x2 v = {lo, hi};
+    if constexpr (DT == NF4DQ_F16) v = opaque2(v);
     if constexpr (DT == NF4DQ_BF16) {
         return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
     } else {
