@@ -286,3 +286,28 @@ def test_persistent_grouped_gemm(coracle, gpu, cfg):
     torch.cuda.synchronize()
     for y, W in zip(ys, Ws):
         _check(y, xb, W, "bf16")
+
+
+def test_quantized_linears_grouped_fp16_bias(gpu):
+    """NF4-quantize real-valued weights (our bitsandbytes-layout quantizer), then the grouped
+    fused path with biases equals per-module dequant + matmul (same dequantized weights)."""
+    from nf4_triton_dequantization import triton_dequantize_nf4
+    from nf4_triton_dequantization_amd import nf4_linear, nf4_linear_grouped
+    from nf4_triton_dequantization_amd.bnb_layout import Linear4bit
+
+    torch.manual_seed(0)
+    K = 2048
+    mods, biases = [], []
+    for N in (1024, 256, 256):
+        lin = Linear4bit(K, N, bias=None, compute_dtype=torch.float16, weight=torch.randn(N, K) * 0.02)
+        mods.append(lin.to(gpu))
+        biases.append((torch.randn(N) * 0.1).to(torch.float16).to(gpu))
+    x = (torch.randn(2, 3, K) * 0.5).to(torch.float16).to(gpu)
+    ys = nf4_linear_grouped(x, mods, biases)
+    for y, mod, b in zip(ys, mods, biases):
+        W = triton_dequantize_nf4(mod).float()
+        ref = x.float() @ W.t() + b.float()
+        assert y.shape == (2, 3, W.shape[0]) and y.dtype == torch.float16
+        assert torch.allclose(y.float(), ref, rtol=2 ** -9, atol=2e-3), (y.float() - ref).abs().max()
+        y1 = nf4_linear(x, mod, bias=b)
+        assert torch.allclose(y.float(), y1.float(), rtol=2 ** -9, atol=2e-3)
