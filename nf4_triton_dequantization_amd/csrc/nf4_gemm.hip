@@ -354,7 +354,8 @@ __device__ __forceinline__ void sslot_issue(const StreamArgs& A, const StreamMat
 template <int DT, int MT>
 __device__ __forceinline__ void sslot_mma(const SSlot& s, uint32_t qa, float qb, const f32x2* ptab,
                                           const float* qtab, const char* smem, uint32_t slot8,
-                                          const uint32_t (&xa)[MT], f32x4 (&acc)[MT]) {
+                                          const uint32_t (&xa)[MT], f32x4 (&acc)[MT], f32x4 (&accb)[MT]) {
+    // even steps accumulate into acc, odd into accb: two MFMA dependency chains of 4
     const float sc = qtab[qa] * qb;  // (:45, :97-98)
     // both halves materialised: a half left to op_sel would read a stale
     // register, and its pending load (as far as the waitcnt pass knows) drains the ring
@@ -390,12 +391,13 @@ __device__ __forceinline__ void sslot_mma(const SSlot& s, uint32_t qa, float qb,
         const u32x4 bq = {bw[0], bw[1], bw[2], bw[3]};
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
+            f32x4& c = (st & 1) ? accb[mt] : acc[mt];
             if constexpr (DT == NF4DQ_BF16) {
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[mt]),
-                                                                  __builtin_bit_cast(bf16x8, bq), acc[mt], 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[mt]),
+                                                            __builtin_bit_cast(bf16x8, bq), c, 0, 0, 0);
             } else {
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[mt]),
-                                                                 __builtin_bit_cast(f16x8, bq), acc[mt], 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[mt]),
+                                                           __builtin_bit_cast(f16x8, bq), c, 0, 0, 0);
             }
         }
     }
@@ -515,9 +517,9 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
         xa0[mt] = live[mt] ? kLdsX + (16u * mt + nl) * A.xstride + kh * 128u : A.zero_off;
     }
     const uint32_t slot8 = (lane & 31u) * 8u;
-    f32x4 acc[MT];
+    f32x4 acc[MT], accb[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = accb[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto body = [&](uint32_t jj, int j, uint32_t qa, float qb) {
         const uint32_t l = l0 + jj;  // chunk within the slice
         uint32_t xa[MT];
@@ -527,7 +529,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
         acc[0][0] += __uint_as_float((ring[j].w0[0] ^ ring[j].w1[3] ^ qa) & 0x3FFFFFFFu) * qb;
         (void)xa;
 #else
-        sslot_mma<DT, MT>(ring[j], qa, qb, ptab, qtab, smem, slot8, xa, acc);
+        sslot_mma<DT, MT>(ring[j], qa, qb, ptab, qtab, smem, slot8, xa, acc, accb);
 #endif
     };
     if constexpr (VS) {
@@ -563,6 +565,8 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
         }
     }
 
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] += accb[mt];
     NF4_STAMP(2);
     // 4. the strip's K parts meet in LDS, in part order (the partials reuse the
     // x slice's LDS once every wave is done reading it)
@@ -740,7 +744,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     const bool live = nl < A.M;
     const uint32_t xa0 = live ? kLdsX + nl * A.xstride + kh * 128u : A.zero_off;
     const uint32_t slot8 = (lane & 31u) * 8u;
-    f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, accb[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
     uint32_t it = 0, rr = 0, buf = 0;
 
     auto round = [&](PScales<P>& cur, PScales<P>& nxt) {
@@ -752,7 +756,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
             const uint32_t l = l0 + rr * P + (uint32_t)s;
             const uint32_t xa[1] = {live ? xa0 + l * 512u : xa0};
             sslot_mma<DT, 1>(ring[s], (cur.a1[s] >> (8u * kh)) & 0xFFu, __uint_as_float(cur.a2[s]), ptab, qtab, smem,
-                             slot8, xa, acc);
+                             slot8, xa, acc, accb);
             __builtin_amdgcn_sched_barrier(0);
             issue_w(ring[s], s, more);
             __builtin_amdgcn_sched_barrier(0);
@@ -760,7 +764,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         advance();
         if (++rr == rounds) {  // group `it` done (uniform)
             f32x4* red = reinterpret_cast<f32x4*>(smem + A.red_off) + buf * (64u * W);
-            red[wave * 64u + lane] = acc[0];
+            red[wave * 64u + lane] = acc[0] + accb[0];
             __syncthreads();
             if (part == 0) {
                 f32x4 sum = red[wave * 64u + lane];
@@ -772,7 +776,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
                     if (m < A.M) o[m * 16u + nl] = (uint16_t)(pack2<DT>(sum[r], 0.0f) & 0xFFFFu);
                 }
             }
-            acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+            acc[0] = accb[0] = f32x4{0.f, 0.f, 0.f, 0.f};
             buf ^= 1u;
             rr = 0;
             ++it;
