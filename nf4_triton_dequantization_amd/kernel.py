@@ -23,7 +23,8 @@ no silent fallback: compute always goes through ``libnf4dq.so``.
 
 Extensions beyond the reference: ``dequantize_nf4_many`` (one
 launch for many weights), ``dequantize_nf4_bnb`` (bitsandbytes semantics,
-parity unpinned) and ``dequantize_nf4_into`` (caller-provided output).
+parity unpinned), ``dequantize_nf4_into`` (caller-provided output) and the
+consumer ``x @ W.t()`` fused: ``nf4_linear`` / ``nf4_linear_grouped``.
 """
 from __future__ import annotations
 
@@ -50,6 +51,15 @@ def _require_device(t: torch.Tensor) -> None:
         # RuntimeError("0 active drivers ..."); there is no CPU path here either.
         raise RuntimeError(
             f"triton_dequantize_nf4: weight is on '{t.device}'; the NF4 HIP path needs a ROCm device tensor")
+
+
+def _on_device(device: torch.device, *tensors: torch.Tensor) -> None:
+    """Quant statistics must live with the packed weight (the reference hands them
+    to Triton, which refuses a host tensor); never pass a host pointer to a kernel."""
+    for t in tensors:
+        if t.device != device:
+            raise RuntimeError(f"NF4 quant state tensor on '{t.device}', packed weight on '{device}': "
+                               f"all of them must be on the same ROCm device")
 
 
 def _stream_ptr(device: torch.device) -> int:
@@ -87,6 +97,7 @@ def _launch(qweight, absmax, absmax32, out, m, n, code, stream) -> None:
     if qweight.dtype != torch.uint8:
         qweight = qweight.to(torch.uint8)  # value cast, as :162-163
     qweight, qp, qn = _flat_ptr(qweight)
+    _on_device(qweight.device, absmax, absmax32 if absmax.dtype == torch.uint8 else absmax)
     L = _lib.lib()
     if absmax.dtype == torch.uint8:
         if absmax32.dtype != torch.float32:
@@ -173,6 +184,7 @@ def dequantize_nf4_many(modules: Iterable) -> List[torch.Tensor]:
         if m == 0 or n == 0:
             continue
         q = _as_u8_flat(qweight)
+        _on_device(q.device, absmax, absmax32)
         a1 = absmax.contiguous().view(-1)
         a2 = absmax32.reshape(-1)
         a2 = (a2 if a2.dtype == torch.float32 else a2.to(torch.float32)).contiguous()
@@ -219,6 +231,7 @@ def dequantize_nf4_bnb(module) -> torch.Tensor:
     stream = _stream_ptr(q.device)
     nested = getattr(qs, "state2", None) is not None and qs.absmax.dtype == torch.uint8
     if nested:
+        _on_device(q.device, qs.absmax, qs.state2.code, qs.state2.absmax)
         a1 = qs.absmax.contiguous().view(-1)
         code2 = qs.state2.code.to(torch.float32).contiguous()
         a2 = qs.state2.absmax.to(torch.float32).contiguous().view(-1)
@@ -228,6 +241,7 @@ def dequantize_nf4_bnb(module) -> torch.Tensor:
                                a2.numel(), ctypes.c_float(off), out.data_ptr(), code, numel, bs,
                                int(qs.state2.blocksize), stream)
     else:
+        _on_device(q.device, qs.absmax)
         am = qs.absmax.to(torch.float32).contiguous().view(-1)
         rc = L.nf4_dequant_bnb_single(q.data_ptr(), am.data_ptr(), am.numel(), out.data_ptr(), code, numel,
                                       bs, stream)
@@ -236,6 +250,14 @@ def dequantize_nf4_bnb(module) -> torch.Tensor:
 
 
 _GEMM_WS = {}
+
+
+def _same_device(x: torch.Tensor, w: torch.Tensor) -> None:
+    # what `x @ W.t()` raises for tensors on different devices (never hand a host
+    # or foreign-device pointer to the kernel)
+    if x.device != w.device:
+        raise RuntimeError(f"Expected all tensors to be on the same device, but found at least two devices, "
+                           f"{w.device} and {x.device}!")
 
 
 def _gemm_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -268,6 +290,7 @@ def nf4_linear(x: torch.Tensor, module, bias: Optional[torch.Tensor] = None) -> 
     """
     qweight, absmax, absmax32, dtype, m, n = _prepare(module)
     _require_device(qweight)
+    _same_device(x, qweight)
     N, K = m, n
     if x.shape[-1] != K:
         raise RuntimeError(f"nf4_linear: x has {x.shape[-1]} features, weight expects {K}")
@@ -285,6 +308,7 @@ def nf4_linear(x: torch.Tensor, module, bias: Optional[torch.Tensor] = None) -> 
             xc = xc.to(dtype)
         xc = xc.contiguous()
         y = torch.empty((M, N), dtype=dtype, device=qweight.device)
+        _on_device(qweight.device, absmax, absmax32)
         L = _lib.lib()
         ws_bytes = L.nf4_gemm_workspace_bytes(M, N, K)
         with torch.cuda.device(qweight.device):
@@ -335,6 +359,7 @@ def nf4_linear_grouped(x: torch.Tensor, modules: Sequence, biases: Optional[Sequ
     if not grouped:
         return [nf4_linear(x, mod, bias=b) for mod, b in zip(modules, biases)]
     _require_device(preps[0][0])
+    _same_device(x, preps[0][0])
     xc = x.reshape(M, K)
     if xc.dtype != dtype:
         xc = xc.to(dtype)
@@ -342,6 +367,7 @@ def nf4_linear_grouped(x: torch.Tensor, modules: Sequence, biases: Optional[Sequ
     ys, keep = [], []
     mats = (_lib.GemmMat * len(modules))()
     for i, (q, a1, a2, _dt, m, _n) in enumerate(preps):
+        _on_device(dev, a1, a2)
         y = torch.empty((M, m), dtype=dtype, device=dev)
         _, qp, qn = _flat_ptr(q)
         _, ap, an = _flat_ptr(a1)

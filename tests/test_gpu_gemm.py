@@ -311,3 +311,16 @@ def test_quantized_linears_grouped_fp16_bias(gpu):
         assert torch.allclose(y.float(), ref, rtol=2 ** -9, atol=2e-3), (y.float() - ref).abs().max()
         y1 = nf4_linear(x, mod, bias=b)
         assert torch.allclose(y.float(), y1.float(), rtol=2 ** -9, atol=2e-3)
+
+
+def test_host_activation_is_rejected(gpu):
+    """x on the host and W on the GPU: RuntimeError (as `x @ W.t()`), never a host pointer in a kernel."""
+    from nf4_triton_dequantization_amd import nf4_linear, nf4_linear_grouped
+
+    packed, a1, a2 = O.make_inputs(128, 256, seed=3)
+    mod = make_module(packed, a1, a2, 128, 256, "bf16", gpu)
+    x = torch.randn(1, 256).to(torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        nf4_linear(x, mod)
+    with pytest.raises(RuntimeError):
+        nf4_linear_grouped(x, [mod, mod])

@@ -279,3 +279,19 @@ def test_double_rounding_and_signed_zero(coracle, gpu, dt, n):
     # the signed zeros are really there
     w = want[-2:].reshape(-1)
     assert (w == 0x8000).any() and (w == 0).any()
+
+
+def test_host_quant_state_is_rejected(gpu):
+    """absmax on the host with the packed weight on the GPU raises (no host pointer reaches a kernel)."""
+    from nf4_triton_dequantization import triton_dequantize_nf4
+    from nf4_triton_dequantization_amd import dequantize_nf4_many, nf4_linear
+
+    packed, a1, a2 = O.make_inputs(64, 128, seed=2)
+    mod = make_module(packed, a1, a2, 64, 128, "bf16", gpu)
+    mod.weight.quant_state.absmax = mod.weight.quant_state.absmax.cpu()
+    with pytest.raises(RuntimeError):
+        triton_dequantize_nf4(mod)
+    with pytest.raises(RuntimeError):
+        dequantize_nf4_many([mod])
+    with pytest.raises(RuntimeError):
+        nf4_linear(torch.zeros(1, 128, dtype=torch.bfloat16, device=gpu), mod)
