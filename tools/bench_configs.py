@@ -10,6 +10,9 @@ c3b  the "4096/11008" shape set BASELINE names (Llama-2-7B: q,k,v,o 4096x4096;
 c4   4096x4096 NF4 -> fp16 vs bf16 vs fp32 output, single launches over 16
      rotating buffer sets, hipGraph replay.
 c5   one 8192x8192 NF4->bf16 matrix (the per-GPU unit of the 8-GPU config).
+bnb  4096x4096 NF4->bf16 with bitsandbytes semantics (nf4_dequant_bnb: code2[A1] * A2
+     + offset, flat blocks), same method as c4; its algorithmic bytes
+     add the 1 KiB nested code book.
 
 Every line: elements/s and algorithmic GB/s (SURVEY §8d bytes) vs the 8 TB/s
 peak; timing = HIP events around the whole pass on the launch stream.
@@ -105,9 +108,31 @@ def run_single(name, m, n, dt, code, reps, dev, sets=16, steps=64):
             "elements_per_s": m * n / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK}
 
 
+def run_bnb(name, m, n, reps, dev, sets=16, steps=64):
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2)
+    ws = [make_weight(m, n, dev, gen, torch.bfloat16) for _ in range(sets)]
+    code2 = torch.linspace(-1, 1, 256, device=dev, dtype=torch.float32)
+    L = _lib.lib()
+    numel = m * n
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        sp = torch.cuda.current_stream().cuda_stream
+        for i in range(steps):
+            q, a1, a2, o = ws[i % sets]
+            assert L.nf4_dequant_bnb(q.data_ptr(), a1.data_ptr(), a1.numel(), code2.data_ptr(), a2.data_ptr(),
+                                     a2.numel(), ctypes.c_float(0.0123), o.data_ptr(), _lib.BF16, numel, 64, 256,
+                                     sp) == 0
+    t = timed(graph.replay, reps) / steps
+    nb = numel // 64
+    byt = numel // 2 + 2 * numel + nb + 4 * ((nb + 255) // 256) + 1024
+    return {"config": name, "m": m, "n": n, "out_dtype": "bfloat16", "us_per_launch": t * 1e6,
+            "elements_per_s": numel / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c3,c3b,c4,c5")
+    ap.add_argument("--configs", default="c3,c3b,c4,c5,bnb")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--layers", type=int, default=32)
     args = ap.parse_args()
@@ -127,6 +152,10 @@ def main():
     if "c5" in todo:
         print(json.dumps(run_single("c5 8192x8192 per-GPU unit", 8192, 8192, torch.bfloat16, _lib.BF16, args.reps, dev,
                                     sets=8, steps=32)), flush=True)
+
+
+    if "bnb" in todo:
+        print(json.dumps(run_bnb("bnb-semantics 4096x4096 NF4->bf16", 4096, 4096, args.reps, dev)), flush=True)
 
 
 if __name__ == "__main__":
