@@ -302,7 +302,8 @@ struct SSlot {
 // body, 2 = the body on register-made data without weight loads, 3 = per-wave
 // s_memrealtime stamps (start, prologue done, loop done, end) into the
 // workspace after the counter region (ksplit 1 only), 4 = no absmax loads,
-// 5 = neither weight loads nor dequant, 6 = no activation loads (x staged from registers).
+// 5 = neither weight loads nor dequant, 6 = no activation loads (x staged from registers),
+// 7 = 5 without the pair-table build (stream kernel).
 #ifndef NF4_STREAM_DEBUG
 #define NF4_STREAM_DEBUG 0
 #endif
@@ -319,7 +320,7 @@ __device__ __forceinline__ void sslot_issue(const StreamArgs& A, const StreamMat
     // the waitcnt pass sees one straight-line ring
     const uint32_t oob = valid ? 0u : kOob;
     const uint32_t woff = (row * (A.K >> 1) + c * 128u + kh * 32u) | oob;
-#if NF4_STREAM_DEBUG == 2 || NF4_STREAM_DEBUG == 5
+#if NF4_STREAM_DEBUG == 2 || NF4_STREAM_DEBUG == 5 || NF4_STREAM_DEBUG == 7
     s.w0 = u32x4{woff, woff * 3u, woff ^ 0x5555u, c};
     s.w1 = u32x4{c * 7u, woff + c, row, kh};
     s.qa = (woff >> 3) & 0xFFu;
@@ -495,11 +496,13 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     // (lo, t) and writes it for all 16 hi -- the hi codes are immediates.
     if (tid < 256u) qtab[tid] = (float)tid / 127.0f;  // IEEE division
     if (tid < 8u) *reinterpret_cast<u32x4*>(smem + A.zero_off + 16u * tid) = u32x4{0u, 0u, 0u, 0u};
+#if NF4_STREAM_DEBUG != 7
     for (uint32_t u = tid; u < 16u * 32u; u += 64u * W) {
         const float clo = nf4_code(u >> 5);
 #pragma unroll
         for (int hi = 0; hi < 16; ++hi) ptab[(16u * hi + (u >> 5)) * 32u + (u & 31u)] = f32x2{nf4_code(hi), clo};
     }
+#endif
 #pragma unroll
     for (int i = 0; i < XR; ++i)
         if (xdst[i] != 0xFFFFFFFFu) *reinterpret_cast<u32x4*>(smem + xdst[i]) = xv[i];
@@ -525,7 +528,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
         uint32_t xa[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) xa[mt] = live[mt] ? xa0[mt] + l * 512u : xa0[mt];
-#if NF4_STREAM_DEBUG == 1 || NF4_STREAM_DEBUG == 4 || NF4_STREAM_DEBUG == 5
+#if NF4_STREAM_DEBUG == 1 || NF4_STREAM_DEBUG == 4 || NF4_STREAM_DEBUG == 5 || NF4_STREAM_DEBUG == 7
         acc[0][0] += __uint_as_float((ring[j].w0[0] ^ ring[j].w1[3] ^ qa) & 0x3FFFFFFFu) * qb;
         (void)xa;
 #else
