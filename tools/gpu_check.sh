@@ -14,7 +14,7 @@ step() {  # step <name> <seconds> <cmd...>
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" >&2; exit $rc; fi
     return 0
 }
-[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=20
+[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 120 --timeout-method thread
 [ "${SKIP_SMOKE:-0}" = 1 ] || step smoke 300 python __graft_entry__.py smoke
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python bench.py ${BENCH_ARGS:-}
 exit 0
