@@ -20,10 +20,11 @@ on the launch stream (region time / K: inter-launch gaps count against us);
 ``peak`` = 8 TB/s; ``traffic`` = PMC-counted HBM bytes per launch from
 profiles/<round>/pmc_traffic.json (tools/pmc_traffic.py) when present.
 
-CPU baseline (``cpu_baseline``, rank 0 at N=1): the C oracle (scalar port of
-the reference fallback, rows split over OpenMP threads = this GPU's host share,
-at most 16) on the same 4096x4096 workload, repeated for ~--cpu-seconds; the
-1-thread figure is reported beside it (``single_thread``).
+CPU baseline (``cpu_baseline``, rank 0 at N=1), same 4096x4096 workload on this
+GPU's host share of cores (at most 16): ``value`` = oracle/fallback_torch.py, a
+torch-CPU restatement with the reference fallback's loop structure (the CPU path
+the reference itself runs); ``native`` = the C oracle over OpenMP threads;
+``single_thread`` = the C oracle on one thread.
 
 Multi-GPU (weak scaling): every rank dequantizes its own matrices; rank 0 owns
 the quant statistics of all ranks' matrices and broadcasts them once over RCCL
@@ -82,36 +83,59 @@ def gen_stats(m, n, seed):
 
 
 def cpu_baseline(m, n, seconds, dtype_code):
-    """Time the C oracle on the same workload: ~`seconds` with one thread per core of
-    this GPU's host share (rows split over OpenMP threads), then ~`seconds`/4 with
-    one thread (the scalar figure, reported alongside)."""
+    """CPU figures on the same workload, on this GPU's host share of cores (<= 16):
+
+    * ``value``: oracle/fallback_torch.py -- torch-CPU restatement with the
+      reference fallback's execution shape (kernel_optimized.py:208-314: per-block
+      scale loop, per-column strided writes), the "reference fallback" row of
+      BASELINE.md's CPU plan; ~`seconds` of repeats;
+    * ``native``: the C oracle, rows over OpenMP threads (~`seconds`/2);
+    * ``single_thread``: the C oracle on one thread (~`seconds`/4).
+    """
     sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import fallback_torch as F
     import nf4_oracle as O
 
     c = O.COracle()
     p, a1, a2 = O.make_inputs(m, n, 3409)
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
 
-    def timed(threads, secs):
-        c.set_threads(threads)
-        c.dequant_ref(p, a1, a2, m, n, dtype_code)  # warm (page-in, thread pool)
+    def repeat(fn, secs):
+        fn()  # warm (page-in, thread pool)
         t0 = time.perf_counter()
         reps = 0
         while True:
-            c.dequant_ref(p, a1, a2, m, n, dtype_code)
+            fn()
             reps += 1
             el = time.perf_counter() - t0
             if el >= secs:
                 return reps, el
 
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
-    reps, el = timed(threads, seconds)
-    reps1, el1 = timed(1, max(1.0, seconds / 4))
+    tdt = torch.bfloat16 if dtype_code == O.BF16 else torch.float16
+    tp, ta1, ta2 = torch.from_numpy(p), torch.from_numpy(a1), torch.from_numpy(a2)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        rf, ef = repeat(lambda: F.dequant_fallback(tp, ta1, ta2, m, n, tdt), seconds)
+    finally:
+        torch.set_num_threads(prev)
+
+    def native(nthreads, secs):
+        c.set_threads(nthreads)
+        return repeat(lambda: c.dequant_ref(p, a1, a2, m, n, dtype_code), secs)
+
+    rn, en = native(threads, max(1.0, seconds / 2))
+    r1, e1 = native(1, max(1.0, seconds / 4))
     c.set_threads(1)
-    return {"value": reps * m * n / el, "unit": "elements/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} x {m}x{n} NF4->bf16 dequant by oracle/nf4_oracle.c (scalar C, rows over "
-                      f"{threads} OpenMP threads), {el:.1f} s",
-            "single_thread": {"value": reps1 * m * n / el1, "cores": 1,
-                              "sample": f"{reps1} x {m}x{n}, 1 thread, {el1:.1f} s"}}
+    dname = "bf16" if dtype_code == O.BF16 else "fp16"
+    return {"value": rf * m * n / ef, "unit": "elements/s", "cores": threads, "kind": "port",
+            "sample": f"{rf} x {m}x{n} NF4->{dname} by oracle/fallback_torch.py (the reference fallback's "
+                      f"loop structure in torch-CPU, {threads} threads), {ef:.1f} s",
+            "native": {"value": rn * m * n / en, "cores": threads,
+                       "sample": f"{rn} x {m}x{n} by oracle/nf4_oracle.c (scalar C, rows over {threads} "
+                                 f"OpenMP threads), {en:.1f} s"},
+            "single_thread": {"value": r1 * m * n / e1, "cores": 1,
+                              "sample": f"{r1} x {m}x{n} by oracle/nf4_oracle.c, 1 thread, {e1:.1f} s"}}
 
 
 def main():

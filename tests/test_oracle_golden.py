@@ -162,3 +162,41 @@ def test_threaded_oracle_is_identical(coracle):
     finally:
         coracle.set_threads(1)
     assert np.array_equal(one, four)
+
+
+def _fallback_case(z, e):
+    import torch
+
+    import fallback_torch as F
+    from _helpers import torch_dtype
+
+    m, n = e["m"], e["n"]
+    packed = torch.from_numpy(z["packed"])
+    if "absmax_f32" in z:
+        absmax, a2 = torch.from_numpy(z["absmax_f32"]), None
+    else:
+        absmax = torch.from_numpy(z["a1"])
+        a2 = torch.from_numpy(z["a2_f16"] if "a2_f16" in z else z["a2"])
+    return F.dequant_fallback(packed, absmax, a2, m, n, torch_dtype(e["dtype"]))
+
+
+def test_fallback_torch_matches_reference_fixtures(manifest):
+    """The bench's fallback-structured CPU figure computes the reference's outputs bit for bit."""
+    from _helpers import out_bits
+
+    for name, e in _small(manifest):
+        z = load_case(e)
+        assert_bits_equal(out_bits(_fallback_case(z, e)), z["out_bits"], e["dtype"], name)
+
+
+def test_fallback_torch_matches_reference_digest_c1(manifest):
+    import torch
+
+    import fallback_torch as F
+    from _helpers import out_bits
+
+    e = manifest["cases"]["C1_1024x1024_f16"]
+    p, a1, a2, _ = O.golden_case_inputs(e["m"], e["n"], e["seed"], e["overrides"])
+    got = F.dequant_fallback(torch.from_numpy(p), torch.from_numpy(a1), torch.from_numpy(a2), e["m"], e["n"],
+                             torch.float16)
+    assert sha(out_bits(got)) == e["sha256"]
