@@ -58,6 +58,7 @@ struct Desc {
     FastDiv bpr;             // blocks per row
     uint32_t blk_shift;      // log2(bytes per scale block)
     uint32_t blk2_shift;     // bnb: log2(blocksize2)
+    uint32_t blk_base;       // scale blocks before this piece (a matrix above kPieceBytes is several pieces)
 };
 
 template <int MAXB>
@@ -140,6 +141,7 @@ __device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rs
     uint32_t g = (base >> bsh) + (bpt ? (lane & (bpt - 1u)) : 0u);
     const uint32_t nblk = (D.nbytes + (1u << bsh) - 1u) >> bsh;
     g = g < nblk ? g : nblk - 1u;  // lanes past the end read a valid block; their stores drop
+    g += D.blk_base;               // block index within the whole matrix / stream
     if constexpr (MODE == kRef) {
         in.a1 = D.a1[fmodu(g, D.nb)];
         const uint32_t r = fdiv(g, D.bpr);
@@ -536,10 +538,64 @@ int check_common(const uint8_t* packed, int64_t packed_len, const void* out, int
 
 // Fill a flat-path descriptor for reference / single semantics, or return false
 // when the matrix needs the rows kernel.
+// Buffer descriptors address < 4 GiB: a flat piece holds < 2^29 packed bytes
+// (2 GiB of 16-bit / 4 GiB of fp32 output).  Bigger matrices (a 70B model's
+// 128256 x 8192 lm_head) go as several row-aligned pieces of one launch, each
+// carrying its first scale block (Desc::blk_base); block indices stay < 2^31.
+constexpr int64_t kPieceBytes = int64_t(1) << 29;
+constexpr int64_t kMaxFlatBlocks = int64_t(1) << 31;
+
 bool flat_eligible(const uint8_t* packed, int64_t packed_len, const void* out, int64_t m, int64_t n) {
-    // buffer descriptors address <= 4 GiB of output: keep packed bytes < 2^29
-    return n % 64 == 0 && packed_len == m * (n / 2) && packed_len < (int64_t(1) << 29) &&
+    return n % 64 == 0 && packed_len == m * (n / 2) && n / 2 < kPieceBytes && packed_len / 32 < kMaxFlatBlocks &&
            aligned(packed, 4) && aligned(out, 16);
+}
+
+// Rows per piece of a flat-eligible matrix with n columns.
+inline int64_t piece_rows(int64_t n) { return (kPieceBytes - 1) / (n / 2); }
+
+// Append the row pieces of one flat-eligible matrix (descriptor `proto` covers
+// the whole matrix) to batch `b`, launching whenever it fills.
+template <int MAXB>
+int append_pieces(Batch<MAXB>& b, const Desc& proto, int64_t m, int64_t n, int32_t dtype, int mode,
+                  hipStream_t st) {
+    const int64_t rows = piece_rows(n);
+    const int64_t ob = dtype == NF4DQ_F32 ? 4 * n : 2 * n;
+    for (int64_t r0 = 0; r0 < m; r0 += rows) {
+        const int64_t r1 = r0 + rows < m ? r0 + rows : m;
+        Desc d = proto;
+        d.packed = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(proto.packed) + r0 * (n / 2));
+        d.out = reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(proto.out) + r0 * ob);
+        d.nbytes = (uint32_t)((r1 - r0) * (n / 2));
+        d.blk_base = (uint32_t)(r0 * (n / 64));
+        d.tile_begin = b.total_tiles;
+        b.d[b.count++] = d;
+        b.total_tiles += (d.nbytes + 1023u) / 1024u;
+        if (b.count == (uint32_t)MAXB || b.total_tiles > (1u << 30)) {
+            const int rc = launch_flat_batch(b, dtype, mode, kDefaultCfg, st);
+            if (rc) return rc;
+            b.count = 0;
+            b.total_tiles = 0;
+        }
+    }
+    return NF4DQ_OK;
+}
+
+// One flat-eligible matrix: a single-descriptor launch, or pieces.
+int launch_flat_matrix(const Desc& proto, int64_t m, int64_t n, int32_t dtype, int mode, const nf4_launch_cfg& cfg,
+                       hipStream_t st) {
+    const int64_t packed_len = m * (n / 2);
+    if (packed_len < kPieceBytes) {
+        Batch<1> b{};
+        b.d[0] = proto;
+        b.d[0].nbytes = (uint32_t)packed_len;
+        b.count = 1;
+        b.total_tiles = (uint32_t)((packed_len + 1023) / 1024);
+        return launch_flat_batch(b, dtype, mode, cfg, st);
+    }
+    Batch<NF4DQ_BATCH_MAX> b{};
+    const int rc = append_pieces(b, proto, m, n, dtype, mode, st);
+    if (rc || b.count == 0) return rc;
+    return launch_flat_batch(b, dtype, mode, kDefaultCfg, st);
 }
 
 Desc ref_desc(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int64_t nb, const float* a2,
@@ -549,7 +605,7 @@ Desc ref_desc(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int6
     d.a1 = a1;
     d.a2 = a2;
     d.out = reinterpret_cast<u32x4*>(out);
-    d.nbytes = (uint32_t)packed_len;
+    d.nbytes = packed_len < kPieceBytes ? (uint32_t)packed_len : 0u;  // pieces set their own
     const int64_t bpr = (n + 63) / 64;
     d.groups = (uint32_t)((bpr + 3) / 4);
     // moduli above 2^31 never wrap for indices < 2^31: clamp keeps FastDiv valid
@@ -565,13 +621,8 @@ int ref_impl(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int64
     int rc = check_common(packed, packed_len, out, dtype, m, n);
     if (rc || m == 0 || n == 0) return rc;
     if (!a1 || !a2 || nb <= 0 || n2 <= 0) return NF4DQ_ERR_ARG;
-    if (flat_eligible(packed, packed_len, out, m, n)) {
-        Batch<1> b{};
-        b.d[0] = ref_desc(packed, packed_len, a1, nb, a2, n2, out, n);
-        b.count = 1;
-        b.total_tiles = (uint32_t)((packed_len + 1023) / 1024);
-        return launch_flat_batch(b, dtype, kRef, cfg, st);
-    }
+    if (flat_eligible(packed, packed_len, out, m, n))
+        return launch_flat_matrix(ref_desc(packed, packed_len, a1, nb, a2, n2, out, n), m, n, dtype, kRef, cfg, st);
     RowsArgs A{};
     A.packed = packed;
     A.a1 = a1;
@@ -630,12 +681,9 @@ int nf4_dequant_single(const uint8_t* packed, int64_t packed_len, const float* a
     if (absmax_len % m || absmax_len / m < bpr) return NF4DQ_ERR_SHAPE;
     const int64_t rs = absmax_len / m;
     if (flat_eligible(packed, packed_len, out, m, n) && absmax_len < (int64_t(1) << 31)) {
-        Batch<1> b{};
-        b.d[0] = ref_desc(packed, packed_len, nullptr, 1, absmax, 1, out, n);
-        b.d[0].n2 = make_fastdiv((uint32_t)rs);
-        b.count = 1;
-        b.total_tiles = (uint32_t)((packed_len + 1023) / 1024);
-        return launch_flat_batch(b, out_dtype, kSingle, kDefaultCfg, st);
+        Desc d = ref_desc(packed, packed_len, nullptr, 1, absmax, 1, out, n);
+        d.n2 = make_fastdiv((uint32_t)rs);
+        return launch_flat_matrix(d, m, n, out_dtype, kSingle, kDefaultCfg, st);
     }
     RowsArgs A{};
     A.packed = packed;
@@ -678,16 +726,9 @@ int nf4_dequant_ref_batched(const nf4_matrix_desc* descs, int32_t count, int32_t
             if (rc) return rc;
             continue;
         }
-        Desc x = ref_desc(d.packed, d.packed_len, d.absmax_q, d.nb, d.absmax2, d.n2, d.out, d.n);
-        x.tile_begin = b.total_tiles;
-        b.d[b.count++] = x;
-        b.total_tiles += (uint32_t)((d.packed_len + 1023) / 1024);
-        if (b.count == NF4DQ_BATCH_MAX || b.total_tiles > (1u << 30)) {
-            int rc = launch_flat_batch(b, out_dtype, kRef, kDefaultCfg, st);
-            if (rc) return rc;
-            b.count = 0;
-            b.total_tiles = 0;
-        }
+        const int rc = append_pieces(b, ref_desc(d.packed, d.packed_len, d.absmax_q, d.nb, d.absmax2, d.n2, d.out,
+                                                 d.n), d.m, d.n, out_dtype, kRef, st);
+        if (rc) return rc;
     }
     if (b.count) return launch_flat_batch(b, out_dtype, kRef, kDefaultCfg, st);
     return NF4DQ_OK;
@@ -709,21 +750,48 @@ static int bnb_common(const uint8_t* packed, const uint8_t* a1, int64_t nb, cons
         if (n2 < (nblk + blocksize2 - 1) / blocksize2) return NF4DQ_ERR_SHAPE;
     }
     const int mode = single ? kBnbSingle : kBnb;
-    if (numel % 8 == 0 && numel / 2 < (int64_t(1) << 29) && aligned(packed, 4) && aligned(out, 16)) {
-        Batch<1> b{};
-        Desc& d = b.d[0];
+    if (numel % 8 == 0 && nblk < kMaxFlatBlocks && blocksize <= (1 << 28) && aligned(packed, 4) && aligned(out, 16)) {
+        // the stream as one matrix of rows of kPieceBytes / 2 packed bytes (a
+        // multiple of every block's byte count): pieces exactly as above
+        const int64_t nbytes = numel / 2;
+        const int64_t row = nbytes < kPieceBytes ? nbytes : kPieceBytes / 2;
+        Desc d{};
         d.packed = reinterpret_cast<const uint32_t*>(packed);
         d.a1 = a1;
         d.a2 = a2;
         d.code2 = code2;
         d.out = reinterpret_cast<u32x4*>(out);
         d.offset = offset;
-        d.nbytes = (uint32_t)(numel / 2);
         d.blk_shift = (uint32_t)ilog2((uint64_t)blocksize / 2);
         d.blk2_shift = single ? 0u : (uint32_t)ilog2((uint64_t)blocksize2);
-        b.count = 1;
-        b.total_tiles = (d.nbytes + 1023u) / 1024u;
-        return launch_flat_batch(b, dtype, mode, kDefaultCfg, st);
+        if (nbytes < kPieceBytes) {
+            Batch<1> b{};
+            b.d[0] = d;
+            b.d[0].nbytes = (uint32_t)nbytes;
+            b.count = 1;
+            b.total_tiles = (uint32_t)((nbytes + 1023) / 1024);
+            return launch_flat_batch(b, dtype, mode, kDefaultCfg, st);
+        }
+        Batch<NF4DQ_BATCH_MAX> b{};
+        const int64_t ob = dtype == NF4DQ_F32 ? 8 : 4;  // output bytes per packed byte
+        for (int64_t p0 = 0; p0 < nbytes; p0 += row) {
+            Desc x = d;
+            const int64_t len = nbytes - p0 < row ? nbytes - p0 : row;
+            x.packed = reinterpret_cast<const uint32_t*>(packed + p0);
+            x.out = reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(out) + p0 * ob);
+            x.nbytes = (uint32_t)len;
+            x.blk_base = (uint32_t)(p0 >> d.blk_shift);
+            x.tile_begin = b.total_tiles;
+            b.d[b.count++] = x;
+            b.total_tiles += (uint32_t)((len + 1023) / 1024);
+            if (b.count == NF4DQ_BATCH_MAX) {
+                const int rc = launch_flat_batch(b, dtype, mode, kDefaultCfg, st);
+                if (rc) return rc;
+                b.count = 0;
+                b.total_tiles = 0;
+            }
+        }
+        return b.count ? launch_flat_batch(b, dtype, mode, kDefaultCfg, st) : NF4DQ_OK;
     }
     BnbBytesArgs A{};
     A.packed = packed;

@@ -173,6 +173,7 @@ int nf4o_dequant_bnb(const uint8_t* packed, const uint8_t* a1, int64_t nb,
     if (blocksize <= 0 || blocksize2 <= 0) return -1;
     if ((numel + blocksize - 1) / blocksize > nb) return -1;
     if (((numel + blocksize - 1) / blocksize + blocksize2 - 1) / blocksize2 > n2) return -1;
+#pragma omp parallel for num_threads(g_threads) schedule(static) if (g_threads > 1)
     for (int64_t k = 0; k < numel; ++k) {
         int64_t blk = k / blocksize;
         float am = code2[a1[blk]] * a2[blk / blocksize2];
@@ -189,6 +190,7 @@ int nf4o_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t 
                             void* out, int dtype, int64_t numel, int64_t blocksize) {
     if (numel <= 0) return 0;
     if (blocksize <= 0 || (numel + blocksize - 1) / blocksize > nabs) return -1;
+#pragma omp parallel for num_threads(g_threads) schedule(static) if (g_threads > 1)
     for (int64_t k = 0; k < numel; ++k) {
         uint8_t byte = packed[k >> 1];
         int nib = (k & 1) ? (byte & 0xF) : (byte >> 4);
