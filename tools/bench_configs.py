@@ -10,12 +10,15 @@ c3b  the "4096/11008" shape set BASELINE names (Llama-2-7B: q,k,v,o 4096x4096;
 c4   4096x4096 NF4 -> fp16 vs bf16 vs fp32 output, single launches over 16
      rotating buffer sets, hipGraph replay.
 c5   one 8192x8192 NF4->bf16 matrix (the per-GPU unit of the 8-GPU config).
+big  128256x8192 NF4->bf16 (Llama-3-70B lm_head size: 525 MB packed, past one buffer
+     descriptor -- two row pieces in one launch).
 bnb  4096x4096 NF4->bf16 with bitsandbytes semantics (nf4_dequant_bnb: code2[A1] * A2
      + offset, flat blocks), same method as c4; its algorithmic bytes
      add the 1 KiB nested code book.
 
 Every line: elements/s and algorithmic GB/s (SURVEY §8d bytes) vs the 8 TB/s
-peak; timing = HIP events around the whole pass on the launch stream.
+peak; timing = HIP events around the whole pass on the launch stream (c3/c3b: the
+pass captured in a hipGraph, the eager figure alongside).
 """
 from __future__ import annotations
 
@@ -81,12 +84,19 @@ def run_model(name, shapes, layers, reps, dev):
         rc = L.nf4_dequant_ref_batched(descs, len(ws), _lib.BF16, torch.cuda.current_stream().cuda_stream)
         assert rc == 0, rc
 
-    t = timed(fn, reps)
+    te = timed(fn, reps)  # eager: host launches inside the timed region
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    t = timed(g.replay, reps)  # the pass captured once (as bench.py times its steps)
     elems = sum(o.numel() for *_, o in ws)
     byt = sum(alg_bytes(o.shape[0], o.shape[1], 2) for *_, o in ws)
     launches = -(-len(ws) // _lib.BATCH_MAX)
     return {"config": name, "matrices": len(ws), "launches": launches, "elements": elems, "seconds": t,
-            "elements_per_s": elems / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK}
+            "elements_per_s": elems / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK,
+            "timing": "hipGraph replay of the pass", "eager_seconds": te, "eager_frac": byt / te / PEAK}
 
 
 def run_single(name, m, n, dt, code, reps, dev, sets=16, steps=64):
@@ -132,7 +142,7 @@ def run_bnb(name, m, n, reps, dev, sets=16, steps=64):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c3,c3b,c4,c5,bnb")
+    ap.add_argument("--configs", default="c3,c3b,c4,c5,big,bnb")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--layers", type=int, default=32)
     args = ap.parse_args()
@@ -154,6 +164,10 @@ def main():
                                     sets=8, steps=32)), flush=True)
 
 
+    if "big" in todo:
+        print(json.dumps(run_single("big 128256x8192 (a 70B lm_head: two flat pieces, one launch)", 128256, 8192,
+                                    torch.bfloat16, _lib.BF16, args.reps, dev, sets=2, steps=8)), flush=True)
+        torch.cuda.empty_cache()
     if "bnb" in todo:
         print(json.dumps(run_bnb("bnb-semantics 4096x4096 NF4->bf16", 4096, 4096, args.reps, dev)), flush=True)
 
