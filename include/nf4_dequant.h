@@ -148,7 +148,7 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
  * NF4DQ_GEMM_STREAM (K % 256 == 0; waves 4/8/16, depth = chunks in flight per
  * wave 2/4/8 (8 not with 16 waves; 16 waves only when M <= 16), strips = 16-column strips per workgroup
  * 1/2/4 dividing waves) or NF4DQ_GEMM_K128 (waves 4/8, depth 1/2/4 (<= 2 when
- * M > 16), strips ignored).  ksplit: K slices reduced across workgroups.
+ * M > 16), strips = 16-column strips per wave 1/2/4 (0 = 1), sharing x loads).  ksplit: K slices reduced across workgroups.
  * NF4DQ_GEMM_PERSIST: the streaming kernel's persistent form (M <= 16,
  * ksplit 1, waves / strips K parts dividing K / 256 into a multiple of depth
  * (2/4), x[M][K] in LDS, absmax not wrapping inside a row).

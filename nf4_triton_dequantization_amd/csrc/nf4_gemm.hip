@@ -37,6 +37,59 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kAuxSc1 = 16;  // write-through stores / L2-bypassing loads (cross-XCD hand-off)
+constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads return 0, stores drop
+
+// The last arriver's split-K sum for one column group of KCOLS columns: slab
+// [ksplit][M][ld] fp32 (sc1-written by every slice), columns col0.. of the
+// slab -> y[m][ycol0 ..] (row stride yld), slices added in slice order (bitwise
+// reproducible).  One wave; every lane owns float4 pieces of the group, and
+// 8 pieces x 4 slices of loads are in flight before any add -- the loads come
+// from another XCD's write-through traffic (L2-missing, ~1-2 us each), so a
+// loop that waits per element would serialise M x KCOLS / 64 of them.
+template <int DT, uint32_t KCOLS>
+__device__ __forceinline__ void splitk_reduce(__amdgpu_buffer_rsrc_t rs, uint32_t ksplit, uint32_t M, uint32_t ld,
+                                              uint32_t col0, void* y, uint32_t yld, uint32_t ycol0, uint32_t lane) {
+    constexpr uint32_t kQ = KCOLS / 4;  // float4 pieces per row
+    constexpr int kU = 8, kK = 4;
+    const uint32_t total = M * kQ;
+    for (uint32_t base = 0; base < total; base += 64u * kU) {
+        f32x4 sum[kU];
+        uint32_t off[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t q = base + lane + 64u * u;
+            const uint32_t m = q / kQ, c = q % kQ;
+            off[u] = q < total ? (m * ld + col0 + 4u * c) * 4u : kOob;
+        }
+        for (uint32_t k0 = 0; k0 < ksplit; k0 += kK) {
+            f32x4 v[kK][kU];
+#pragma unroll
+            for (int j = 0; j < kK; ++j)
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const uint32_t k = k0 + j;
+                    const uint32_t o = k < ksplit && off[u] != kOob ? off[u] + k * M * ld * 4u : kOob;
+                    v[j][u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, kAuxSc1));
+                }
+#pragma unroll
+            for (int j = 0; j < kK; ++j) {
+                if (k0 + j >= ksplit) break;  // uniform
+#pragma unroll
+                for (int u = 0; u < kU; ++u) sum[u] = (k0 + j == 0) ? v[j][u] : sum[u] + v[j][u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t q = base + lane + 64u * u;
+            if (q < total) {
+                const uint32_t m = q / kQ, c = q % kQ;
+                uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(y) + m * yld + ycol0 + 4u * c);
+                dst[0] = pack2<DT>(sum[u][0], sum[u][1]);
+                dst[1] = pack2<DT>(sum[u][2], sum[u][3]);
+            }
+        }
+    }
+}
 
 template <int DT>
 __device__ __forceinline__ void store_y(void* y, uint32_t i, float v) {
@@ -65,23 +118,28 @@ struct GemmArgs {
     FastDiv nb, n2;
 };
 
-// One 128-deep K chunk of one lane: 16 packed weight bytes of its row (one
-// 64-block, so one scale) and MT x 4 activation fragments.
-template <int MT>
+// One 128-deep K chunk of one lane: for each of the wave's NT 16-column strips,
+// 16 packed weight bytes of its row there (one 64-block, so one scale), and
+// MT x 4 activation fragments -- shared by the NT strips, so a wider wave
+// (NT > 1) loads x once per NT weights instead of once per weight.
+template <int MT, int NT>
 struct Chunk {
-    u32x4 w;
-    uint32_t qa;    // absmax byte
-    float qb;       // nested absmax
+    u32x4 w[NT];
+    uint32_t qa[NT];    // absmax bytes
+    float qb[NT];       // nested absmax
     u32x4 x[MT][4];
 };
 
-template <int MT>
+template <int MT, int NT>
 __device__ __forceinline__ void chunk_issue(const GemmArgs& A, __amdgpu_buffer_rsrc_t rw, __amdgpu_buffer_rsrc_t rx,
                                             uint32_t c, bool valid, uint32_t row, uint32_t nl, uint32_t kh,
-                                            Chunk<MT>& in) {
+                                            Chunk<MT, NT>& in) {
     const uint32_t kbase = c * kChunkK + 32u * kh;
     // past the wave's last chunk: offsets beyond the buffer ranges (zeros, no traffic)
-    in.w = __builtin_amdgcn_raw_buffer_load_b128(rw, valid ? row * (A.K >> 1) + (kbase >> 1) : 0xFFFFFFF0u, 0, 0);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+        in.w[nt] = __builtin_amdgcn_raw_buffer_load_b128(
+            rw, valid ? (row + 16u * nt) * (A.K >> 1) + (kbase >> 1) : 0xFFFFFFF0u, 0, 0);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
         const uint32_t xoff = valid ? ((16u * mt + nl) * A.K + kbase) * 2u : 0xFFFFFF00u;  // rows >= M: zeros
@@ -89,45 +147,52 @@ __device__ __forceinline__ void chunk_issue(const GemmArgs& A, __amdgpu_buffer_r
         for (int s = 0; s < 4; ++s) in.x[mt][s] = __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + 16u * s, 0, 0);
     }
     const uint32_t b = 2u * (valid ? c : 0u) + (kh >> 1);  // 64-block within the row
-    in.qa = A.a1[fmodu(row * A.bpr + b, A.nb)];               // (:173-177 wrap)
-    in.qb = A.a2[fmodu(row * A.groups + (b >> 2), A.n2)];    // (:40-41, :183-186 wrap)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const uint32_t r = row + 16u * nt;
+        in.qa[nt] = A.a1[fmodu(r * A.bpr + b, A.nb)];             // (:173-177 wrap)
+        in.qb[nt] = A.a2[fmodu(r * A.groups + (b >> 2), A.n2)];  // (:40-41, :183-186 wrap)
+    }
 }
 
-template <int DT, int MT>
-__device__ __forceinline__ void chunk_mma(const Chunk<MT>& in, const float* lut, f32x4 (&acc)[MT]) {
-    const float sc = ((float)in.qa / 127.0f) * in.qb;  // IEEE division, then fp32 multiply (:45)
+template <int DT, int MT, int NT>
+__device__ __forceinline__ void chunk_mma(const Chunk<MT, NT>& in, const float* lut, f32x4 (&acc)[MT][NT]) {
     const char* t = reinterpret_cast<const char*>(lut);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const uint32_t wd = in.w[s];
-        const uint32_t hi4 = (wd >> 2) & 0x3C3C3C3Cu;
-        const uint32_t lo4 = (wd << 2) & 0x3C3C3C3Cu;
-        float v[8];
+    for (int nt = 0; nt < NT; ++nt) {
+        const float sc = ((float)in.qa[nt] / 127.0f) * in.qb[nt];  // IEEE division, then fp32 multiply (:45)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            v[2 * k] = *reinterpret_cast<const float*>(t + ((hi4 >> (8 * k)) & 0xFFu)) * sc;
-            v[2 * k + 1] = *reinterpret_cast<const float*>(t + ((lo4 >> (8 * k)) & 0xFFu)) * sc;
-        }
-        // the exact weights nf4_dequant_ref writes: fp32 product, RNE to 16 bits
-        const u32x4 bw = {pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]),
-                          pack2<DT>(v[6], v[7])};
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t wd = in.w[nt][s];
+            const uint32_t hi4 = (wd >> 2) & 0x3C3C3C3Cu;
+            const uint32_t lo4 = (wd << 2) & 0x3C3C3C3Cu;
+            float v[8];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            if constexpr (DT == NF4DQ_BF16) {
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, in.x[mt][s]),
-                                                                  __builtin_bit_cast(bf16x8, bw), acc[mt], 0, 0, 0);
-            } else {
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, in.x[mt][s]),
-                                                                 __builtin_bit_cast(f16x8, bw), acc[mt], 0, 0, 0);
+            for (int k = 0; k < 4; ++k) {
+                v[2 * k] = *reinterpret_cast<const float*>(t + ((hi4 >> (8 * k)) & 0xFFu)) * sc;
+                v[2 * k + 1] = *reinterpret_cast<const float*>(t + ((lo4 >> (8 * k)) & 0xFFu)) * sc;
+            }
+            // the exact weights nf4_dequant_ref writes: fp32 product, RNE to 16 bits
+            const u32x4 bw = {pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]),
+                              pack2<DT>(v[6], v[7])};
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                if constexpr (DT == NF4DQ_BF16) {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8, in.x[mt][s]), __builtin_bit_cast(bf16x8, bw), acc[mt][nt], 0, 0, 0);
+                } else {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                        __builtin_bit_cast(f16x8, in.x[mt][s]), __builtin_bit_cast(f16x8, bw), acc[mt][nt], 0, 0, 0);
+                }
             }
         }
     }
 }
 
-// Workgroup = WV waves owning 16 output columns of one K slice; wave w takes
-// every WV-th group of D chunks, D chunks in flight at a time; the waves'
-// partial sums are combined through LDS (fixed order).
-template <int DT, int MT, int D, int WV>
+// Workgroup = WV waves owning 16 NT output columns (NT strips) of one K slice;
+// wave w takes every WV-th group of D chunks, D chunks in flight at a time; the
+// waves' partial sums are combined through LDS (fixed order, one strip at a time).
+template <int DT, int MT, int D, int WV, int NT>
 __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs A) {
     constexpr int kGemmWaves = WV;
     __shared__ __attribute__((aligned(16))) float lut[20];  // 16 codes + the last-arriver flag
@@ -135,53 +200,63 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t nl = lane & 15u, kh = lane >> 4;
-    const uint32_t cg = blockIdx.x % A.col_groups;   // 16-column strip
+    const uint32_t cg = blockIdx.x % A.col_groups;   // group of NT 16-column strips
     const uint32_t ks = blockIdx.x / A.col_groups;   // K slice
-    const uint32_t row = cg * 16u + nl;
+    const uint32_t row = cg * 16u * NT + nl;         // this lane's row in strip 0; strip nt adds 16 nt
     const uint32_t c0 = ks * A.chunks_per_split;
     const uint32_t c1 = c0 + A.chunks_per_split < A.chunks ? c0 + A.chunks_per_split : A.chunks;
 
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.N * (A.K >> 1), kRsrcFlags);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
 
-    f32x4 acc[MT];
+    f32x4 acc[MT][NT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     bool first = true;
     for (uint32_t g = c0 + wave * D; g < c1 || first; g += kGemmWaves * D) {
-        Chunk<MT> ch[D];
+        Chunk<MT, NT> ch[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) chunk_issue<MT>(A, rw, rx, g + d, g + d < c1, row, nl, kh, ch[d]);
+        for (int d = 0; d < D; ++d) chunk_issue<MT, NT>(A, rw, rx, g + d, g + d < c1, row, nl, kh, ch[d]);
         if (first) {  // LUT + barrier overlap the first loads
             write_lut(lut);
             __syncthreads();
             first = false;
         }
 #pragma unroll
-        for (int d = 0; d < D; ++d) chunk_mma<DT, MT>(ch[d], lut, acc);
+        for (int d = 0; d < D; ++d) chunk_mma<DT, MT, NT>(ch[d], lut, acc);
     }
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[mt];
-    __syncthreads();
-    if (wave != 0) return;
+    for (int nt = 0; nt < NT; ++nt) {
+        if (nt) __syncthreads();  // wave 0 has read the previous strip's partials
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        f32x4 s = red[0][mt][lane];
+        for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[mt][nt];
+        __syncthreads();
+        if (wave == 0) {
 #pragma unroll
-        for (int w = 1; w < kGemmWaves; ++w) s += red[w][mt][lane];
-        acc[mt] = s;
-    }
-
-    // acc[mt][r] = Y[16 mt + 4 kh + r][n0 + nl]
-    if (A.ksplit == 1) {
+            for (int mt = 0; mt < MT; ++mt) {
+                f32x4 s = red[0][mt][lane];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t m = 16u * mt + 4u * kh + r;
-                if (m < A.M) store_y<DT>(A.y, m * A.N + row, acc[mt][r]);
+                for (int w = 1; w < kGemmWaves; ++w) s += red[w][mt][lane];
+                acc[mt][nt] = s;
             }
         }
+    }
+    if (wave != 0) return;
+
+    // acc[mt][nt][r] = Y[16 mt + 4 kh + r][row + 16 nt]
+    if (A.ksplit == 1) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t m = 16u * mt + 4u * kh + r;
+                    if (m < A.M) store_y<DT>(A.y, m * A.N + row + 16u * nt, acc[mt][nt][r]);
+                }
+            }
         return;
     }
 
@@ -194,14 +269,16 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)A.slab, 0, A.ksplit * A.M * A.N * 4u, kRsrcFlags);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t m = 16u * mt + 4u * kh + r;
-            const uint32_t off = m < A.M ? ((ks * A.M + m) * A.N + row) * 4u : 0xFFFFFFF0u;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][r]), rs, off, 0, kAuxSc1);
+        for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t m = 16u * mt + 4u * kh + r;
+                const uint32_t off = m < A.M ? ((ks * A.M + m) * A.N + row + 16u * nt) * 4u : 0xFFFFFFF0u;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][nt][r]), rs, off, 0, kAuxSc1);
+            }
         }
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // only wave 0 is left: its own drain is the hand-off
     uint32_t last = 0;
     if (lane == 0) {
@@ -212,16 +289,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     }
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
-    for (uint32_t i = lane; i < A.M * 16u; i += 64u) {
-        const uint32_t m = i >> 4;
-        const uint32_t n = cg * 16u + (i & 15u);
-        float sum = 0.0f;
-        for (uint32_t k = 0; k < A.ksplit; ++k) {
-            sum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ((k * A.M + m) * A.N + n) * 4u, 0,
-                                                                        kAuxSc1));
-        }
-        store_y<DT>(A.y, m * A.N + n, sum);
-    }
+    splitk_reduce<DT, 16u * NT>(rs, A.ksplit, A.M, A.N, cg * 16u * NT, A.y, A.N, cg * 16u * NT, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -308,7 +376,6 @@ struct SSlot {
 #define NF4_STREAM_DEBUG 0
 #endif
 
-constexpr uint32_t kOob = 0x80000000u;
 constexpr int kVsMax = 16;  // chunks per wave covered by the vector-scale form  // beyond every buffer range: loads return 0, no traffic
 
 template <bool VS>
@@ -619,15 +686,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     }
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
-    for (uint32_t i = lane; i < A.M * 16u; i += 64u) {
-        const uint32_t m = i >> 4;
-        const uint32_t c = i & 15u;
-        float sum = 0.0f;
-        for (uint32_t k = 0; k < A.ksplit; ++k)
-            sum += __uint_as_float(
-                __builtin_amdgcn_raw_buffer_load_b32(rs, ((k * A.M + m) * A.ncols + gstrip * 16u + c) * 4u, 0, kAuxSc1));
-        store_y<DT>(Mt.y, m * Mt.N + strip * 16u + c, sum);
-    }
+    splitk_reduce<DT, 16u>(rs, A.ksplit, A.M, A.ncols, gstrip * 16u, Mt.y, Mt.N, strip * 16u, lane);
 }
 
 
@@ -833,36 +892,58 @@ static bool stream_fits(int64_t M, int64_t K, const nf4_gemm_cfg& c) {
     return p.lds <= kStreamLdsCap && M * (int64_t)p.cps * 32 <= xr * 64 * c.waves;
 }
 
-// Defaults, from tools/sweep_gemm.py on MI355X (Llama-3-8B shapes, M = 1, 4, 16, 32):
-// the streaming kernel for decode-sized M (8 waves, 2 chunks in flight, whole K
-// per workgroup; 4 strips per workgroup for wide N; a 2-way K split for long K
-// once M > 1), the 128-deep kernel for 16 < M and for narrow N at M = 16.
+// Defaults, from tools/sweep_gemm.py on MI355X (profiles/r01/sweep_gemm.jsonl:
+// Llama-3-8B shapes and the grouped q/k/v and gate/up column totals, M = 1..32).
+// N = all columns of the launch (a grouped launch passes the sum).
+//  * M <= 8: the persistent streaming kernel whenever x[M][K] fits its LDS
+//    (falls back to the streaming kernel if absmax wraps inside a row), strips
+//    by width; long K (down projection): streaming, K split growing with M.
+//  * 8 < M <= 16: streaming with a 2-way K split and 4 strips per workgroup for
+//    wide N; the 128-deep kernel for narrow N and long K.
+//  * 16 < M <= 32: the 128-deep kernel with several strips per wave (x loads
+//    shared) and a K split where N alone cannot fill the chip.
 bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K);
 
-nf4_gemm_cfg default_gemm_cfg(int64_t M, int64_t N, int64_t K) {
-    // N = all columns of the launch (a grouped launch passes the sum)
-    if (K % kSChunkK == 0 && (M <= 8 || (M <= 16 && N >= 8192))) {
-        nf4_gemm_cfg c{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};
-        if (M > 8) {
-            c.ksplit = 2;
-            c.strips = 4;
-        } else if (K >= 8192) {
-            if (M > 1) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 2, 2};
-        } else if (N >= 16384) {
-            c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 4, 2, 1, 4};
-        } else if (N >= 8192) {
-            c.strips = 4;
-        } else if (N > 4096) {  // q/k/v-sized launches: persistent form (falls back if absmax wraps in a row)
-            c = nf4_gemm_cfg{NF4DQ_GEMM_PERSIST, 8, 2, 1, 2};
-        } else if (K == 4096) {
-            c.kernel = NF4DQ_GEMM_PERSIST;
-        }
-        if (c.kernel == NF4DQ_GEMM_PERSIST && !valid_gemm_cfg(c, M, N, K)) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};
-        while (c.ksplit < K / kSChunkK && !stream_fits(M, K, c)) ++c.ksplit;
-        return c;
-    }
-    nf4_gemm_cfg c{NF4DQ_GEMM_K128, 8, M > 16 ? 1 : 2, 1, 1};
+static nf4_gemm_cfg k128_cfg(int64_t M, int64_t N, int64_t K, int waves, int depth, int ksplit, int strips) {
+    nf4_gemm_cfg c{NF4DQ_GEMM_K128, waves, depth, ksplit, strips};
+    if (M > 16 && c.depth > 2) c.depth = 2;
+    while (c.strips > 1 && N % (16 * c.strips)) c.strips /= 2;
+    if (c.ksplit > K / kChunkK) c.ksplit = (int)(K / kChunkK);
+    if (c.ksplit < 1) c.ksplit = 1;
     return c;
+}
+
+nf4_gemm_cfg default_gemm_cfg(int64_t M, int64_t N, int64_t K) {
+    const bool k256 = K % kSChunkK == 0;
+    if (k256 && M <= 8) {
+        const int strips = N >= 16384 ? 1 : N >= 8192 ? 4 : N > 4096 ? 2 : 1;
+        nf4_gemm_cfg c{NF4DQ_GEMM_PERSIST, 8, 2, 1, strips};
+        if (valid_gemm_cfg(c, M, N, K)) return c;
+        if (M == 1) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};
+        else if (M <= 4) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 2, 2};
+        else c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 4, 4};
+        while (c.strips > 1 && N % (16 * c.strips)) c.strips /= 2;
+        if (c.ksplit > K / kSChunkK) c.ksplit = (int)(K / kSChunkK);
+        while (c.ksplit < K / kSChunkK && !stream_fits(M, K, c)) ++c.ksplit;
+        if (valid_gemm_cfg(c, M, N, K)) return c;
+        return k128_cfg(M, N, K, 8, 2, 1, 1);
+    }
+    if (M <= 16) {
+        if (k256 && K < 8192 && N > 4096) {
+            nf4_gemm_cfg c{NF4DQ_GEMM_STREAM, 8, 2, 2, 4};
+            while (c.strips > 1 && N % (16 * c.strips)) c.strips /= 2;
+            while (c.ksplit < K / kSChunkK && !stream_fits(M, K, c)) ++c.ksplit;
+            if (valid_gemm_cfg(c, M, N, K)) return c;
+        }
+        if (K >= 8192) return k128_cfg(M, N, K, 8, 1, 2, 2);
+        if (N < 4096) return k128_cfg(M, N, K, 4, 2, 4, 1);
+        return k128_cfg(M, N, K, 8, 2, 1, 1);
+    }
+    if (K >= 8192) return k128_cfg(M, N, K, 8, 1, 4, 4);
+    if (N < 4096) return k128_cfg(M, N, K, 4, 2, 4, 1);
+    if (N <= 4096) return k128_cfg(M, N, K, 8, 1, 2, 2);
+    if (N < 8192) return k128_cfg(M, N, K, 4, 1, 4, 2);
+    return k128_cfg(M, N, K, N >= 16384 ? 4 : 8, 1, 1, 4);
 }
 
 static uint32_t persist_dyn_bytes(int64_t M, int64_t K, const nf4_gemm_cfg& c, uint32_t groups_per_wg) {
@@ -895,6 +976,7 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
     }
     if (c.kernel != NF4DQ_GEMM_K128) return false;
     if (c.waves != 4 && c.waves != 8) return false;
+    if (c.strips != 0 && c.strips != 1 && c.strips != 2 && c.strips != 4) return false;  // strips per wave
     if (M > 16 ? (c.depth != 1 && c.depth != 2) : (c.depth != 1 && c.depth != 2 && c.depth != 4)) return false;
     return c.ksplit >= 1 && c.ksplit <= K / kChunkK && c.ksplit <= 64;
 }
@@ -1159,7 +1241,6 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     A.M = (uint32_t)M;
     A.N = (uint32_t)N;
     A.K = (uint32_t)K;
-    A.col_groups = (uint32_t)(N / 16);
     A.ksplit = ks;
     A.chunks = (uint32_t)(K / kChunkK);
     A.chunks_per_split = (A.chunks + ks - 1) / ks;
@@ -1167,13 +1248,22 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     A.groups = (A.bpr + 3) / 4;
     A.nb = make_fastdiv((uint32_t)(nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : nb));
     A.n2 = make_fastdiv((uint32_t)(n2 > (int64_t(1) << 31) ? (int64_t(1) << 31) : n2));
+    const int nt = cfg.strips > 1 ? cfg.strips : 1;  // 16-column strips per wave
+    A.col_groups = (uint32_t)(N / (16 * nt));
     const dim3 grid(A.col_groups * ks), block(64 * cfg.waves);
     const int mt = (int)((M + 15) / 16);
-#define NF4_G(DT_, MT_, D_, W_) hipLaunchKernelGGL((nf4_gemm_smallm_kernel<DT_, MT_, D_, W_>), grid, block, 0, st, A)
+#define NF4_G(DT_, MT_, D_, W_, NT_) \
+    hipLaunchKernelGGL((nf4_gemm_smallm_kernel<DT_, MT_, D_, W_, NT_>), grid, block, 0, st, A)
+#define NF4_N(DT_, MT_, D_, W_)                   \
+    do {                                          \
+        if (nt == 4) NF4_G(DT_, MT_, D_, W_, 4);  \
+        else if (nt == 2) NF4_G(DT_, MT_, D_, W_, 2); \
+        else NF4_G(DT_, MT_, D_, W_, 1);          \
+    } while (0)
 #define NF4_W(DT_, MT_, D_)                        \
     do {                                           \
-        if (cfg.waves == 8) NF4_G(DT_, MT_, D_, 8); \
-        else NF4_G(DT_, MT_, D_, 4);               \
+        if (cfg.waves == 8) NF4_N(DT_, MT_, D_, 8); \
+        else NF4_N(DT_, MT_, D_, 4);               \
     } while (0)
 #define NF4_S(DT_)                                  \
     do {                                            \
@@ -1190,6 +1280,7 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     else NF4_S(NF4DQ_F16);
 #undef NF4_S
 #undef NF4_W
+#undef NF4_N
 #undef NF4_G
     return hip_rc2(hipGetLastError());
 }

@@ -168,7 +168,7 @@ def test_every_decomposition_agrees_with_oracle(coracle, gpu, dt, M, N, K):
     for kernel in (_lib.GEMM_PERSIST, _lib.GEMM_STREAM, _lib.GEMM_K128):
         for waves in (4, 8, 16):
             for depth in (1, 2, 4, 8):
-                for strips in ((1, 2, 4) if kernel != _lib.GEMM_K128 else (1,)):
+                for strips in (1, 2, 4):  # K128: strips per wave
                     for ks in (1, 3):
                         cfg = _lib.GemmCfg(kernel, waves, depth, ks, strips)
                         y.fill_(float("nan"))
@@ -191,7 +191,7 @@ def test_invalid_decompositions_rejected(gpu):
     F = 0x1000
     for cfg in [(_lib.GEMM_STREAM, 6, 4, 1, 1), (_lib.GEMM_STREAM, 8, 3, 1, 1), (_lib.GEMM_STREAM, 8, 4, 1, 3),
                 (_lib.GEMM_STREAM, 4, 4, 1, 8), (_lib.GEMM_STREAM, 8, 4, 0, 1), (_lib.GEMM_STREAM, 8, 4, 99, 1),
-                (_lib.GEMM_K128, 16, 2, 1, 1), (7, 8, 4, 1, 1)]:
+                (_lib.GEMM_K128, 16, 2, 1, 1), (_lib.GEMM_K128, 8, 2, 1, 3), (7, 8, 4, 1, 1)]:
         c = _lib.GemmCfg(*cfg)
         assert L.nf4_gemm_ref_cfg(F, 1, F, 64 * 2048, F, 64 * 64, F, 16, F, _lib.BF16, 64, 4096, F, 1 << 30,
                                   ctypes.byref(c), None) == _lib.ERR_ARG, cfg

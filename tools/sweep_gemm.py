@@ -21,7 +21,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 from nf4_triton_dequantization_amd import _lib  # noqa: E402
 
-SHAPES = [(4096, 4096), (1024, 4096), (14336, 4096), (4096, 14336)]
+SHAPES = [(4096, 4096), (1024, 4096), (14336, 4096), (4096, 14336), (6144, 4096), (28672, 4096)]
+# (6144, 4096) / (28672, 4096): the column totals of the grouped q/k/v and gate/up
+# launches (default_gemm_cfg is keyed by the launch's total N)
 
 
 def graph_us(fn, n_launch, reps=5):
@@ -74,12 +76,13 @@ def main():
             for waves in (4, 8, 16):
                 for depth in (2, 4, 8):
                     for strips in (1, 2, 4):
-                        for ks in (1, 2, 4):
+                        for ks in (1, 2, 4, 8):
                             cfgs.append(_lib.GemmCfg(_lib.GEMM_STREAM, waves, depth, ks, strips))
-            for waves in (8,):
+            for waves in (4, 8):
                 for depth in (1, 2):
-                    for ks in (1, 2):
-                        cfgs.append(_lib.GemmCfg(_lib.GEMM_K128, waves, depth, ks, 1))
+                    for strips in (1, 2, 4):  # K128: strips per wave
+                        for ks in (1, 2, 4, 8):
+                            cfgs.append(_lib.GemmCfg(_lib.GEMM_K128, waves, depth, ks, strips))
             for cfg in cfgs:
                 wsz = L.nf4_gemm_workspace_bytes_cfg(M, n, k, ctypes.byref(cfg))
                 work = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=dev)
@@ -121,7 +124,7 @@ def main():
             res.sort(key=lambda r: r["us"])
             print(json.dumps({"N": n, "K": k, "M": M, "copies": copies, "default_us": round(dus, 2),
                               "default_TBps": round(wbytes / dus / 1e6, 3), "best": res[:8],
-                              "worst": res[-2:]}), flush=True)
+                              "worst": res[-2:], "all": res}), flush=True)
         del ws
         torch.cuda.empty_cache()
 
