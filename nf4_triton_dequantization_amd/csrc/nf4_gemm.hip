@@ -718,7 +718,7 @@ struct PGeo {  // where the ring issues: one strip of one weight
     uint32_t row, b1, b2;
 };
 
-template <int DT, int W, int P>
+template <int DT, int W, int P, bool SPLIT>
 __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamArgs A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ __attribute__((aligned(16))) f32x2 ptab[256 * 32];
@@ -727,14 +727,18 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t nl = lane & 15u, kh = lane >> 4;
     const uint32_t strip_in = wave % A.T, part = wave / A.T;
-    const uint32_t G = gridDim.x;
-    const uint32_t mine = A.sg_total > blockIdx.x ? (A.sg_total - blockIdx.x + G - 1u) / G : 0u;
-    const uint32_t cnt = A.cpp;  // chunks per wave per group (host: parts * cnt == chunks, cnt % P == 0)
+    // K slices: workgroup b works on slice b % ksplit (its x slice staged once),
+    // walking the strip groups b / ksplit, + G / ksplit, ...
+    const uint32_t KS = SPLIT ? A.ksplit : 1u, ks = SPLIT ? blockIdx.x % KS : 0u;
+    const uint32_t G = gridDim.x / KS, j0 = blockIdx.x / KS;
+    const uint32_t mine = A.sg_total > j0 ? (A.sg_total - j0 + G - 1u) / G : 0u;
+    const uint32_t cnt = A.cpp;  // chunks per wave per group (host: parts * cnt == cps, cnt % P == 0)
     const uint32_t rounds = cnt / P, total = mine * rounds;
-    const uint32_t l0 = part * cnt;
+    const uint32_t l0 = part * cnt;          // first chunk of this wave within the slice
+    const uint32_t cbase = ks * A.cps;       // first chunk of the slice within K
 
     auto geo = [&](uint32_t it, PGeo& g) {
-        const uint32_t sgi = blockIdx.x + it * G;
+        const uint32_t sgi = j0 + it * G;
         uint32_t mi = 0;
         for (uint32_t i = 1; i < A.nmat; ++i) mi = sgi >= A.mat[i].sg_begin ? i : mi;
         const StreamMat& Mt = A.mat[mi];
@@ -742,8 +746,8 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         g.rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);
         g.ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a1, 0, Mt.nb_bytes, kRsrcFlags);
         g.ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a2, 0, Mt.n2_bytes, kRsrcFlags);
-        g.b1 = fmodu(g.row * A.bpr, Mt.nb) + 4u * l0;   // reference wrap (:173-186), none inside a row
-        g.b2 = fmodu(g.row * A.groups, Mt.n2) + l0;
+        g.b1 = fmodu(g.row * A.bpr, Mt.nb) + 4u * (cbase + l0);  // reference wrap (:173-186), none inside a row
+        g.b2 = fmodu(g.row * A.groups, Mt.n2) + cbase + l0;
     };
     // issue pointer: group it2, round rr2 of it
     PGeo gi;
@@ -755,7 +759,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         sc.a2 = pload<P>(gi.ra2, ((gi.b2 + P * rr2) * 4u) | oob);
     };
     auto issue_w = [&](SSlot& sl, int s, bool valid) {
-        const uint32_t c = l0 + rr2 * P + (uint32_t)s;
+        const uint32_t c = cbase + l0 + rr2 * P + (uint32_t)s;
         const uint32_t woff = (gi.row * (A.K >> 1) + c * 128u + kh * 32u) | (valid ? 0u : kOob);
         sl.w0 = __builtin_amdgcn_raw_buffer_load_b128(gi.rw, woff, 0, 0);
         sl.w1 = __builtin_amdgcn_raw_buffer_load_b128(gi.rw, woff + 16u, 0, 0);
@@ -769,7 +773,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     };
 
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
-    // 1. x rows (whole K), then round 0 of the ring
+    // 1. x rows (the slice's K range), then round 0 of the ring
     const uint32_t pieces = A.M * A.ppr.d;
     u32x4 xv[kXR];
     uint32_t xdst[kXR];
@@ -777,9 +781,11 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     for (int i = 0; i < kXR; ++i) {
         const uint32_t p = tid + (uint32_t)i * 64u * W;
         const uint32_t r = fdiv(p, A.ppr), q = p - r * A.ppr.d;
-        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, p < pieces ? r * A.K * 2u + q * 16u : kOob, 0, 0);
+        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, p < pieces ? r * A.K * 2u + cbase * 512u + q * 16u : kOob,
+                                                      0, 0);
         xdst[i] = p < pieces ? kLdsX + r * A.xstride + q * 16u : 0xFFFFFFFFu;
     }
+    __builtin_amdgcn_sched_barrier(0);  // x loads first: the staging below must not wait on the ring
     PScales<P> sc[2];
     SSlot ring[P];
     issue_scales(sc[0], total > 0);
@@ -831,11 +837,21 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
             if (part == 0) {
                 f32x4 sum = red[wave * 64u + lane];
                 for (uint32_t q = 1; q < A.parts; ++q) sum += red[(wave + q * A.T) * 64u + lane];
-                uint16_t* o = reinterpret_cast<uint16_t*>(smem + A.out_off) + ((it * A.T + strip_in) * A.M) * 16u;
+                const uint32_t o0 = ((it * A.T + strip_in) * A.M) * 16u;
+                if constexpr (!SPLIT) {  // finished: the 16-bit outputs
+                    uint16_t* o = reinterpret_cast<uint16_t*>(smem + A.out_off) + o0;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const uint32_t m = 4u * kh + r;
-                    if (m < A.M) o[m * 16u + nl] = (uint16_t)(pack2<DT>(sum[r], 0.0f) & 0xFFFFu);
+                    for (int r = 0; r < 4; ++r) {
+                        const uint32_t m = 4u * kh + r;
+                        if (m < A.M) o[m * 16u + nl] = (uint16_t)(pack2<DT>(sum[r], 0.0f) & 0xFFFFu);
+                    }
+                } else {  // this slice's fp32 partial sums
+                    float* o = reinterpret_cast<float*>(smem + A.out_off) + o0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const uint32_t m = 4u * kh + r;
+                        if (m < A.M) o[m * 16u + nl] = sum[r];
+                    }
                 }
             }
             acc[0] = accb[0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -850,17 +866,59 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     }
     // 3. the workgroup's outputs
     __syncthreads();
-    const uint16_t* o = reinterpret_cast<const uint16_t*>(smem + A.out_off);
     const uint32_t per = A.T * A.M * 16u;
-    for (uint32_t i = tid; i < mine * per; i += 64u * W) {
+    if constexpr (!SPLIT) {
+        const uint16_t* o = reinterpret_cast<const uint16_t*>(smem + A.out_off);
+        for (uint32_t i = tid; i < mine * per; i += 64u * W) {
+            const uint32_t ito = i / per, rem = i - ito * per;
+            const uint32_t t = rem / (A.M * 16u), rem2 = rem - t * (A.M * 16u);
+            const uint32_t sgi = j0 + ito * G;
+            uint32_t mi = 0;
+            for (uint32_t j = 1; j < A.nmat; ++j) mi = sgi >= A.mat[j].sg_begin ? j : mi;
+            const StreamMat& Mt = A.mat[mi];
+            const uint32_t col = ((sgi - Mt.sg_begin) * A.T + t) * 16u + (rem2 & 15u);
+            reinterpret_cast<uint16_t*>(Mt.y)[(rem2 >> 4) * Mt.N + col] = o[i];
+        }
+    } else {
+    // 3b. K slices: the partials to the slab [ksplit][M][ncols] (write-through
+    // stores, drained), then per strip group a ticket; the slice drawing
+    // ksplit - 1 sums all slices in slice order (nf4_gemm_smallm_kernel's hand-off)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)A.slab, 0, KS * A.M * A.ncols * 4u, kRsrcFlags);
+    const float* o32 = reinterpret_cast<const float*>(smem + A.out_off);
+    for (uint32_t i = 4u * tid; i < mine * per; i += 4u * 64u * W) {
         const uint32_t ito = i / per, rem = i - ito * per;
         const uint32_t t = rem / (A.M * 16u), rem2 = rem - t * (A.M * 16u);
-        const uint32_t sgi = blockIdx.x + ito * G;
+        const uint32_t sgi = j0 + ito * G;
         uint32_t mi = 0;
         for (uint32_t j = 1; j < A.nmat; ++j) mi = sgi >= A.mat[j].sg_begin ? j : mi;
         const StreamMat& Mt = A.mat[mi];
-        const uint32_t col = ((sgi - Mt.sg_begin) * A.T + t) * 16u + (rem2 & 15u);
-        reinterpret_cast<uint16_t*>(Mt.y)[(rem2 >> 4) * Mt.N + col] = o[i];
+        const uint32_t gstrip = Mt.strip_begin + (sgi - Mt.sg_begin) * A.T + t;
+        const uint32_t off = ((ks * A.M + (rem2 >> 4)) * A.ncols + gstrip * 16u + (rem2 & 15u)) * 4u;
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(o32 + i), rs, off, 0, kAuxSc1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (uint32_t ito = wave; ito < mine; ito += W) {
+        const uint32_t sgi = j0 + ito * G;
+        uint32_t last = 0;
+        if (lane == 0) {
+            const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[sgi], 1u, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+            last = ticket == KS - 1u;
+            if (last) __hip_atomic_store(&A.counters[sgi], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        last = __builtin_amdgcn_readfirstlane(last);
+        if (!last) continue;
+        uint32_t mi = 0;
+        for (uint32_t j = 1; j < A.nmat; ++j) mi = sgi >= A.mat[j].sg_begin ? j : mi;
+        const StreamMat& Mt = A.mat[mi];
+        const uint32_t s0 = (sgi - Mt.sg_begin) * A.T;  // first strip of the group within the weight
+        const uint32_t col0 = (Mt.strip_begin + s0) * 16u;
+        if (A.T == 4) splitk_reduce<DT, 64u>(rs, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
+        else if (A.T == 2) splitk_reduce<DT, 32u>(rs, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
+        else splitk_reduce<DT, 16u>(rs, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
+    }
     }
 }
 
@@ -913,15 +971,14 @@ static nf4_gemm_cfg k128_cfg(int64_t M, int64_t N, int64_t K, int waves, int dep
     return c;
 }
 
-nf4_gemm_cfg default_gemm_cfg(int64_t M, int64_t N, int64_t K) {
+// The library's choice when the persistent kernel is not used (or cannot run:
+// absmax wrapping inside a row, held outputs beyond its LDS).
+static nf4_gemm_cfg nonpersist_cfg(int64_t M, int64_t N, int64_t K) {
     const bool k256 = K % kSChunkK == 0;
     if (k256 && M <= 8) {
-        const int strips = N >= 16384 ? 1 : N >= 8192 ? 4 : N > 4096 ? 2 : 1;
-        nf4_gemm_cfg c{NF4DQ_GEMM_PERSIST, 8, 2, 1, strips};
-        if (valid_gemm_cfg(c, M, N, K)) return c;
-        if (M == 1) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};
-        else if (M <= 4) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 2, 2};
-        else c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 4, 4};
+        nf4_gemm_cfg c{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};
+        if (M > 4) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 4, 4};
+        else if (M > 1) c = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 2, 2};
         while (c.strips > 1 && N % (16 * c.strips)) c.strips /= 2;
         if (c.ksplit > K / kSChunkK) c.ksplit = (int)(K / kSChunkK);
         while (c.ksplit < K / kSChunkK && !stream_fits(M, K, c)) ++c.ksplit;
@@ -946,9 +1003,30 @@ nf4_gemm_cfg default_gemm_cfg(int64_t M, int64_t N, int64_t K) {
     return k128_cfg(M, N, K, N >= 16384 ? 4 : 8, 1, 1, 4);
 }
 
+nf4_gemm_cfg default_gemm_cfg(int64_t M, int64_t N, int64_t K) {
+    if (K % kSChunkK == 0 && M <= 8) {
+        const int strips = N >= 16384 ? 1 : N >= 8192 ? 4 : N > 4096 ? 2 : 1;
+        const nf4_gemm_cfg c{NF4DQ_GEMM_PERSIST, 8, 2, 1, strips};
+        if (valid_gemm_cfg(c, M, N, K)) return c;
+    } else if (K % kSChunkK == 0 && M <= 16) {
+        // persistent with K slices: the fewest slices whose x fits, while the
+        // (strip group, slice) pairs still cover every CU
+        for (int strips = 2; strips <= 4; strips *= 2)
+            for (int ks = 2; ks <= 16; ++ks) {
+                const nf4_gemm_cfg c{NF4DQ_GEMM_PERSIST, 8, 2, ks, strips};
+                if (N / (16 * strips) * ks >= 256 && valid_gemm_cfg(c, M, N, K)) return c;
+            }
+    }
+    return nonpersist_cfg(M, N, K);
+}
+
+// Dynamic LDS of the persistent kernel: x slice, zero block, two partial-sum
+// sets, the held outputs (16-bit finished values; fp32 partials when K is split).
 static uint32_t persist_dyn_bytes(int64_t M, int64_t K, const nf4_gemm_cfg& c, uint32_t groups_per_wg) {
-    const uint32_t xstride = (uint32_t)K * 2u + 16u;
-    const uint32_t out = (groups_per_wg * (uint32_t)c.strips * (uint32_t)M * 32u + 15u) & ~15u;
+    const uint32_t ks = c.ksplit > 1 ? (uint32_t)c.ksplit : 1u;
+    const uint32_t xstride = (uint32_t)(K / ks) * 2u + 16u;
+    const uint32_t ob = ks > 1 ? 64u : 32u;  // bytes per held row of a strip
+    const uint32_t out = (groups_per_wg * (uint32_t)c.strips * (uint32_t)M * ob + 15u) & ~15u;
     return kLdsX + (uint32_t)M * xstride + 128u + 2u * (uint32_t)c.waves * 1024u + out;
 }
 
@@ -958,10 +1036,12 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
         if (c.waves != 4 && c.waves != 8 && c.waves != 16) return false;
         if (c.depth != 2 && c.depth != 4) return false;
         if (c.strips != 1 && c.strips != 2 && c.strips != 4) return false;
-        if (c.waves % c.strips || N % (16 * c.strips) || c.ksplit != 1) return false;
+        if (c.waves % c.strips || N % (16 * c.strips) || c.ksplit < 1 || c.ksplit > 16) return false;
         const int64_t chunks = K / kSChunkK, parts = c.waves / c.strips;
-        if (chunks % parts || (chunks / parts) % c.depth) return false;
-        if (M * (K / 8) > (int64_t)kXR * 64 * c.waves) return false;
+        if (chunks % c.ksplit) return false;
+        const int64_t cps = chunks / c.ksplit;  // chunks per K slice
+        if (cps % parts || (cps / parts) % c.depth) return false;
+        if (M * cps * 32 > (int64_t)kXR * 64 * c.waves) return false;
         return persist_dyn_bytes(M, K, c, 1) + kStreamStatic <= kLdsPerCu;
     }
     if (c.kernel == NF4DQ_GEMM_STREAM) {
@@ -1119,22 +1199,25 @@ static int launch_stream(const HostMat* mats, int count, const void* x, int64_t 
 // One launch of the persistent kernel over `count` weights sharing x (cfg
 // validated per weight).  Grid: as many workgroups as fit the CUs at once.
 static int launch_persist(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
-                          const nf4_gemm_cfg& cfg, hipStream_t st) {
+                          const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st) {
     StreamArgs S{};
+    const uint32_t ks = (uint32_t)cfg.ksplit;
     S.nmat = (uint32_t)count;
     S.x = x;
+    S.counters = reinterpret_cast<uint32_t*>(workspace);
+    S.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
     S.M = (uint32_t)M;
     S.K = (uint32_t)K;
     S.T = (uint32_t)cfg.strips;
     S.parts = (uint32_t)(cfg.waves / cfg.strips);
-    S.ksplit = 1;
+    S.ksplit = ks;
     S.chunks = (uint32_t)(K / kSChunkK);
-    S.cps = S.chunks;
-    S.cpp = S.chunks / S.parts;
+    S.cps = S.chunks / ks;
+    S.cpp = S.cps / S.parts;
     S.bpr = (uint32_t)(K / 64);
     S.groups = (S.bpr + 3) / 4;
-    S.ppr = make_fastdiv((uint32_t)(K / 8));
-    S.xstride = (uint32_t)K * 2u + 16u;
+    S.ppr = make_fastdiv(S.cps * 32u);
+    S.xstride = S.cps * 512u + 16u;
     uint32_t sg = 0, strips = 0;
     for (int i = 0; i < count; ++i) {
         const HostMat& h = mats[i];
@@ -1160,26 +1243,34 @@ static int launch_persist(const HostMat* mats, int count, const void* x, int64_t
     }
     S.sg_total = sg;
     S.ncols = strips * 16u;
+    if (ks > 1 && sg * 4u > kCounterBytes) return NF4DQ_ERR_TOO_LARGE;  // one ticket per strip group
     const uint32_t base = persist_dyn_bytes(M, K, cfg, 1) + kStreamStatic;
     const uint32_t per_cu = kLdsPerCu / base > 0 ? kLdsPerCu / base : 1u;
-    uint32_t G = (uint32_t)device_cus() * per_cu;
-    if (G > sg) G = sg;
-    const uint32_t per_wg = (sg + G - 1) / G;
+    uint32_t G = (uint32_t)device_cus() * per_cu;  // workgroups; G / ks per K slice
+    if (G > sg * ks) G = sg * ks;
+    G = G / ks * ks;
+    if (G < ks) G = ks;
+    const uint32_t per_wg = (sg + G / ks - 1) / (G / ks);
     const uint32_t dyn = persist_dyn_bytes(M, K, cfg, per_wg);
     if (dyn + kStreamStatic > kLdsPerCu) return NF4DQ_ERR_TOO_LARGE;
     S.zero_off = kLdsX + (uint32_t)M * S.xstride;
     S.red_off = S.zero_off + 128u;
     S.out_off = S.red_off + 2u * (uint32_t)cfg.waves * 1024u;
     const dim3 grid(G), block(64 * cfg.waves);
-#define NF4_PK(DT_, W_, P_)                                                                                    \
-    do {                                                                                                       \
-        static bool attr_ = false;                                                                             \
-        if (!attr_) {                                                                                          \
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_persist_kernel<DT_, W_, P_>),    \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsCap);         \
-            attr_ = true;                                                                                      \
-        }                                                                                                      \
-        hipLaunchKernelGGL((nf4_gemm_persist_kernel<DT_, W_, P_>), grid, block, dyn, st, S);                  \
+#define NF4_PK1(DT_, W_, P_, SP_)                                                                               \
+    do {                                                                                                        \
+        static bool attr_ = false;                                                                              \
+        if (!attr_) {                                                                                           \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_persist_kernel<DT_, W_, P_, SP_>), \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsCap);          \
+            attr_ = true;                                                                                       \
+        }                                                                                                       \
+        hipLaunchKernelGGL((nf4_gemm_persist_kernel<DT_, W_, P_, SP_>), grid, block, dyn, st, S);              \
+    } while (0)
+#define NF4_PK(DT_, W_, P_)                        \
+    do {                                           \
+        if (ks > 1) NF4_PK1(DT_, W_, P_, true);    \
+        else NF4_PK1(DT_, W_, P_, false);          \
     } while (0)
 #define NF4_PW(DT_)                                            \
     do {                                                       \
@@ -1198,6 +1289,7 @@ static int launch_persist(const HostMat* mats, int count, const void* x, int64_t
     else NF4_PW(NF4DQ_F16);
 #undef NF4_PW
 #undef NF4_PK
+#undef NF4_PK1
     return hip_rc2(hipGetLastError());
 }
 
@@ -1223,10 +1315,18 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     if (cfg.kernel == NF4DQ_GEMM_STREAM || cfg.kernel == NF4DQ_GEMM_PERSIST) {
         const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
         if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
-            const int rc = launch_persist(&h, 1, x, M, K, dtype, cfg, st);
-            if (rc != NF4DQ_ERR_ARG || cfgp) return rc;
-            cfg = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};  // library choice, absmax wrapping in a row
-            if (!valid_gemm_cfg(cfg, M, N, K)) return NF4DQ_ERR_ARG;
+            const int rc = launch_persist(&h, 1, x, M, K, dtype, cfg, workspace, st);
+            if ((rc != NF4DQ_ERR_ARG && rc != NF4DQ_ERR_TOO_LARGE) || cfgp) return rc;
+            // library choice that cannot run here (absmax wrapping in a row, held
+            // outputs beyond LDS): the next choice; its workspace need is covered
+            // (callers size the workspace with nf4_gemm_workspace_bytes = the max)
+            cfg = nonpersist_cfg(M, N, K);
+            const size_t w2 = workspace_for(M, N, K, cfg);
+            if (!valid_gemm_cfg(cfg, M, N, K) || (w2 && (!workspace || workspace_bytes < w2 || !aligned16(workspace))))
+                return NF4DQ_ERR_ARG;
+            if (cfg.kernel == NF4DQ_GEMM_K128)
+                return gemm_impl(x, M, packed, packed_len, absmax_q, nb, absmax2, n2, y, dtype, N, K, workspace,
+                                 workspace_bytes, &cfg, st);
         }
         return launch_stream(&h, 1, x, M, K, dtype, cfg, workspace, st);
     }
@@ -1329,11 +1429,17 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
         h[i] = HostMat{mats[i].packed, mats[i].packed_len, mats[i].absmax_q, mats[i].nb, mats[i].absmax2,
                        mats[i].n2, mats[i].y, mats[i].N};
     if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
-        const int rc = launch_persist(h, count, x, M, K, dtype, cfg, st);
-        if (rc != NF4DQ_ERR_ARG || cfgp) return rc;
-        cfg = nf4_gemm_cfg{NF4DQ_GEMM_STREAM, 8, 2, 1, 1};  // library choice, absmax wrapping in a row
-        for (int i = 0; i < count; ++i)
-            if (!valid_gemm_cfg(cfg, M, mats[i].N, K)) return NF4DQ_ERR_ARG;
+        const int rc = launch_persist(h, count, x, M, K, dtype, cfg, workspace, st);
+        if ((rc != NF4DQ_ERR_ARG && rc != NF4DQ_ERR_TOO_LARGE) || cfgp) return rc;
+        // library choice that cannot run here: per-weight launches with each weight's own choice
+        for (int i = 0; i < count; ++i) {
+            const nf4_gemm_mat& m = mats[i];
+            nf4_gemm_cfg c = nonpersist_cfg(M, m.N, K);
+            const int r2 = gemm_impl(x, M, m.packed, m.packed_len, m.absmax_q, m.nb, m.absmax2, m.n2, m.y, dtype, m.N,
+                                     K, workspace, workspace_bytes, &c, st);
+            if (r2) return r2;
+        }
+        return NF4DQ_OK;
     }
     return launch_stream(h, count, x, M, K, dtype, cfg, workspace, st);
 }
@@ -1349,11 +1455,16 @@ static size_t grouped_workspace(int64_t M, int64_t K, const nf4_gemm_mat* mats, 
     if (ntot <= 0) return 0;
     nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, ntot, K);
     if (cfg.kernel == 0) cfg.kernel = default_gemm_cfg(M, ntot, K).kernel;
-    if (cfg.kernel == NF4DQ_GEMM_STREAM || cfg.kernel == NF4DQ_GEMM_PERSIST)
-        return cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
-    size_t w = 0;  // per-weight launches: the largest of their needs
+    size_t w = 0;
+    if (cfg.kernel == NF4DQ_GEMM_STREAM || cfg.kernel == NF4DQ_GEMM_PERSIST) {
+        w = cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
+        if (cfgp || cfg.kernel == NF4DQ_GEMM_STREAM) return w;
+    }
+    // per-weight launches (the 128-deep kernel, or the library's fallback from
+    // the persistent kernel): the largest of their needs
     for (int i = 0; i < count; ++i) {
-        const nf4_gemm_cfg c = cfgp ? *cfgp : default_gemm_cfg(M, mats[i].N, K);
+        const nf4_gemm_cfg c = cfgp ? *cfgp : (cfg.kernel == NF4DQ_GEMM_PERSIST ? nonpersist_cfg(M, mats[i].N, K)
+                                                                                : default_gemm_cfg(M, mats[i].N, K));
         const size_t wi = workspace_for(M, mats[i].N, K, c);
         w = wi > w ? wi : w;
     }
@@ -1367,7 +1478,10 @@ extern "C" {
 
 size_t nf4_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K) {
     if (M <= 0 || N <= 0 || K <= 0 || N % 64 || K % kChunkK) return 0;
-    return workspace_for(M, N, K, default_gemm_cfg(M, N, K));
+    // the library's choice, or the next one if that cannot run (see gemm_impl)
+    const size_t a = workspace_for(M, N, K, default_gemm_cfg(M, N, K));
+    const size_t b = workspace_for(M, N, K, nonpersist_cfg(M, N, K));
+    return a > b ? a : b;
 }
 
 size_t nf4_gemm_workspace_bytes_cfg(int64_t M, int64_t N, int64_t K, const nf4_gemm_cfg* cfg) {

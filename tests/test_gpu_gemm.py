@@ -84,6 +84,28 @@ def test_wrapping_absmax_and_leading_dims(coracle, gpu):
     _check(y.reshape(6, N), xb, W, "bf16")
 
 
+@pytest.mark.parametrize("M", [4, 12, 16])
+def test_library_choice_falls_back_when_absmax_wraps_in_a_row(coracle, gpu, M):
+    """At these M the library picks the persistent kernel (K-sliced above 8 rows), which
+    needs absmax without wrap inside a row; with a wrapping absmax (nb = 7, n2 = 3) it must
+    fall back to the next choice -- single weight and grouped -- not fail."""
+    from nf4_triton_dequantization_amd import nf4_linear, nf4_linear_grouped
+
+    K = 4096
+    Ns = (4096, 2048)
+    mods, Ws = [], []
+    for i, N in enumerate(Ns):
+        packed, a1, a2, _ = O.golden_case_inputs(N, K, 40 + i, {"nb": 7 + i, "n2": 3})
+        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16))
+        mods.append(make_module(packed, a1, a2, N, K, "bf16", gpu))
+    xt, xb = _x_bits(M, K, "bf16", seed=M)
+    x = xt.to(gpu)
+    for mod, W in zip(mods, Ws):
+        _check(nf4_linear(x, mod), xb, W, "bf16")
+    for y, W in zip(nf4_linear_grouped(x, mods), Ws):
+        _check(y, xb, W, "bf16")
+
+
 def test_large_m_takes_composite_path(coracle, gpu):
     from nf4_triton_dequantization_amd import nf4_linear
 
@@ -169,7 +191,7 @@ def test_every_decomposition_agrees_with_oracle(coracle, gpu, dt, M, N, K):
         for waves in (4, 8, 16):
             for depth in (1, 2, 4, 8):
                 for strips in (1, 2, 4):  # K128: strips per wave
-                    for ks in (1, 3):
+                    for ks in (1, 2, 3):
                         cfg = _lib.GemmCfg(kernel, waves, depth, ks, strips)
                         y.fill_(float("nan"))
                         rc = _gemm_cfg_call(L, _lib, x, t, y, code, N, K, cfg)
@@ -255,16 +277,19 @@ def test_grouped_gemm_split_k_and_wrapping(coracle, gpu):
             _check(y, xb, W, "bf16")
 
 
-@pytest.mark.parametrize("cfg", [(8, 2, 1), (4, 2, 2), (8, 4, 2), (16, 2, 2), (4, 4, 4)])
+@pytest.mark.parametrize("cfg", [(8, 2, 1, 1, 3), (4, 2, 2, 1, 3), (8, 4, 2, 1, 3), (16, 2, 2, 1, 3), (4, 4, 4, 1, 3),
+                                 (8, 2, 4, 2, 16), (8, 2, 2, 2, 9), (8, 2, 4, 4, 16), (4, 2, 2, 4, 12),
+                                 (16, 2, 4, 2, 5), (4, 2, 4, 8, 16)])
 def test_persistent_grouped_gemm(coracle, gpu, cfg):
-    """The persistent kernel over a grouped launch (several weights, several strip groups per workgroup)."""
+    """The persistent kernel over a grouped launch (several weights, several strip groups per
+    workgroup), whole K or K slices (fp32 partials held in LDS, then the ticketed slab sum)."""
     import ctypes
 
     from nf4_triton_dequantization_amd import _lib
 
     L = _lib.lib()
-    waves, depth, strips = cfg
-    M, K = 3, 4096  # 16 chunks: every cfg above splits them into a multiple of its depth
+    waves, depth, strips, ks, M = cfg
+    K = 4096  # 16 chunks: every cfg above splits them into a multiple of its depth
     Ns = (4096, 1024, 2048)
     mats = (_lib.GemmMat * len(Ns))()
     ys, keep, Ws = [], [], []
@@ -279,13 +304,21 @@ def test_persistent_grouped_gemm(coracle, gpu, cfg):
                                t[2].numel(), y.data_ptr(), N)
     xt, xb = _x_bits(M, K, "bf16", seed=4)
     x = xt.to(gpu)
-    c = _lib.GemmCfg(_lib.GEMM_PERSIST, waves, depth, 1, strips)
-    rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, mats, len(Ns), _lib.BF16, None, 0, ctypes.byref(c),
-                                torch.cuda.current_stream().cuda_stream)
-    assert rc == 0, rc
-    torch.cuda.synchronize()
-    for y, W in zip(ys, Ws):
-        _check(y, xb, W, "bf16")
+    c = _lib.GemmCfg(_lib.GEMM_PERSIST, waves, depth, ks, strips)
+    wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, mats, len(Ns), ctypes.byref(c))
+    assert (wsz > 0) == (ks > 1)
+    ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=gpu)
+    for _ in range(2):  # the second call reuses the tickets the first left at 0
+        for y in ys:
+            y.fill_(float("nan"))
+        rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, mats, len(Ns), _lib.BF16, ws.data_ptr() if wsz else None,
+                                    wsz, ctypes.byref(c), torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+        for y, W in zip(ys, Ws):
+            _check(y, xb, W, "bf16")
+    if ks > 1:
+        assert int(ws[:65536].view(torch.int32).abs().sum()) == 0  # tickets back at 0
 
 
 def test_quantized_linears_grouped_fp16_bias(gpu):

@@ -58,7 +58,11 @@ def main():
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--ms", default="1,4,8,16,32")
     ap.add_argument("--no-bf16", action="store_true")
+    ap.add_argument("--no-composite", action="store_true")
+    ap.add_argument("--lib", default="prod", help="prod, or a tools/_build/libnf4dq_<name>.so variant (A/B runs)")
     args = ap.parse_args()
+    if args.lib != "prod":
+        _lib.LIB_PATH = os.path.join(REPO, "tools", "_build", f"libnf4dq_{args.lib}.so")
     dev = torch.device("cuda", 0)
     L = _lib.lib()
     gen = torch.Generator(device=dev)
@@ -136,10 +140,12 @@ def main():
         tg = graph_ms(grouped)
         res.update({"grouped_ms": tg, "grouped_TBps": (packed_bytes + io_bytes) / (tg * 1e-3) / 1e12,
                     "grouped_launches": len(groups)})
-        res["composite_ms"] = graph_ms(composite)
+        res["lib"] = args.lib
+        if not args.no_composite:
+            res["composite_ms"] = graph_ms(composite)
+            res["speedup_vs_composite"] = res["composite_ms"] / t
         if wbf is not None:
             res["bf16_weights_ms"] = graph_ms(bf16)
-        res["speedup_vs_composite"] = res["composite_ms"] / t
         if wbf is not None:
             res["speedup_vs_bf16_weights"] = res["bf16_weights_ms"] / t
         print(json.dumps(res), flush=True)

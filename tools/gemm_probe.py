@@ -50,6 +50,13 @@ def main():
             cfg = _lib.GemmCfg(*(int(v) for v in cs.split(",")))
             wsz = L.nf4_gemm_workspace_bytes_cfg(M, n, k, ctypes.byref(cfg))
             work = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=dev)
+            q0, a10, a20 = ws[0]
+            rc0 = L.nf4_gemm_ref_cfg(x.data_ptr(), M, q0.data_ptr(), q0.numel(), a10.data_ptr(), a10.numel(),
+                                     a20.data_ptr(), a20.numel(), y.data_ptr(), _lib.BF16, n, k, work.data_ptr(), wsz,
+                                     ctypes.byref(cfg), torch.cuda.current_stream().cuda_stream)
+            if rc0 != 0:  # not a valid decomposition for this shape
+                print(json.dumps({"lib": args.lib, "N": n, "K": k, "M": M, "cfg": cs, "rc": rc0}), flush=True)
+                continue
 
             def run(cfg=cfg, work=work, wsz=wsz):
                 sp = torch.cuda.current_stream().cuda_stream
