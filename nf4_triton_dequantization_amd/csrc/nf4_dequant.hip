@@ -425,6 +425,15 @@ int launch_tuned(const Batch<MAXB>& b, uint64_t blocks, uint32_t U, bool ntl, in
     if (U == 8) {
         if (ntl) NF4_W(8, kAuxNt);
         else NF4_W(8, 0);
+    } else if (U == 2 || U == 1) {  // finer pipeline steps (experiment): default-policy loads only
+        if (ntl) return NF4DQ_ERR_ARG;
+        if (U == 2) {
+            if (wpg == 8) NF4_T(2, 0, 8);
+            else NF4_T(2, 0, 4);
+        } else {
+            if (wpg == 8) NF4_T(1, 0, 8);
+            else NF4_T(1, 0, 4);
+        }
     } else {
         if (ntl) NF4_W(4, kAuxNt);
         else NF4_W(4, 0);
@@ -437,7 +446,7 @@ int launch_tuned(const Batch<MAXB>& b, uint64_t blocks, uint32_t U, bool ntl, in
 template <int MAXB>
 int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_launch_cfg& cfg, hipStream_t st) {
     if (bt.count == 0) return NF4DQ_OK;
-    const uint32_t U = cfg.tile_dwords == 8 ? 8u : 4u;
+    const uint32_t U = cfg.tile_dwords == 8 ? 8u : cfg.tile_dwords == 2 ? 2u : cfg.tile_dwords == 1 ? 1u : 4u;
     const bool ntl = (cfg.flags & NF4DQ_CFG_NT_LOADS) != 0;
     const int wpg_log = (int)((cfg.flags >> NF4DQ_CFG_WG_SHIFT_BIT) & 0xF);
     const int wpg = wpg_log ? (1 << wpg_log) : 4;
@@ -497,6 +506,7 @@ int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_laun
         else launch_one<NF4DQ_F16, kRef, 4, 0, 0, 4, MAXB>(b, blocks, st);
         if (U != 4 || ntl || wpg != 4) return NF4DQ_ERR_ARG;  // default-policy stores: base shape only
     } else if (tuned) {
+        if (U < 4 && (ntl || (wpg != 4 && wpg != 8))) return NF4DQ_ERR_ARG;
         if (dtype == NF4DQ_BF16) launch_tuned<NF4DQ_BF16>(b, blocks, U, ntl, wpg, st);
         else launch_tuned<NF4DQ_F16>(b, blocks, U, ntl, wpg, st);
     } else {
@@ -658,7 +668,9 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len, const uint8_t
                         const float* absmax2, int64_t n2, void* out, int32_t out_dtype, int64_t m, int64_t n,
                         const nf4_launch_cfg* cfg, void* hip_stream) {
     nf4_launch_cfg c = cfg ? *cfg : kDefaultCfg;
-    if (c.tile_dwords != 4 && c.tile_dwords != 8) return NF4DQ_ERR_ARG;
+    if (c.tile_dwords != 1 && c.tile_dwords != 2 && c.tile_dwords != 4 && c.tile_dwords != 8) return NF4DQ_ERR_ARG;
+    if (c.tile_dwords < 4 && (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_STORE_POLICY_MASK)))
+        return NF4DQ_ERR_ARG;
     if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_SEG_SHIFT_MASK | NF4DQ_CFG_WG_SHIFT_MASK |
                     NF4DQ_CFG_STORE_POLICY_MASK))
         return NF4DQ_ERR_ARG;
