@@ -130,7 +130,8 @@ struct Chunk {
     u32x4 x[MT][4];
 };
 
-template <int MT, int NT>
+// VS: the block scales come from the workgroup's LDS table (nf4_gemm_smallm_kernel), no per-chunk gathers
+template <int MT, int NT, bool VS>
 __device__ __forceinline__ void chunk_issue(const GemmArgs& A, __amdgpu_buffer_rsrc_t rw, __amdgpu_buffer_rsrc_t rx,
                                             uint32_t c, bool valid, uint32_t row, uint32_t nl, uint32_t kh,
                                             Chunk<MT, NT>& in) {
@@ -146,21 +147,24 @@ __device__ __forceinline__ void chunk_issue(const GemmArgs& A, __amdgpu_buffer_r
 #pragma unroll
         for (int s = 0; s < 4; ++s) in.x[mt][s] = __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + 16u * s, 0, 0);
     }
-    const uint32_t b = 2u * (valid ? c : 0u) + (kh >> 1);  // 64-block within the row
+    if constexpr (!VS) {
+        const uint32_t b = 2u * (valid ? c : 0u) + (kh >> 1);  // 64-block within the row
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const uint32_t r = row + 16u * nt;
-        in.qa[nt] = A.a1[fmodu(r * A.bpr + b, A.nb)];             // (:173-177 wrap)
-        in.qb[nt] = A.a2[fmodu(r * A.groups + (b >> 2), A.n2)];  // (:40-41, :183-186 wrap)
+        for (int nt = 0; nt < NT; ++nt) {
+            const uint32_t r = row + 16u * nt;
+            in.qa[nt] = A.a1[fmodu(r * A.bpr + b, A.nb)];             // (:173-177 wrap)
+            in.qb[nt] = A.a2[fmodu(r * A.groups + (b >> 2), A.n2)];  // (:40-41, :183-186 wrap)
+        }
     }
 }
 
 template <int DT, int MT, int NT>
-__device__ __forceinline__ void chunk_mma(const Chunk<MT, NT>& in, const float* lut, f32x4 (&acc)[MT][NT]) {
+__device__ __forceinline__ void chunk_mma(const Chunk<MT, NT>& in, const float* lut, const float (&scs)[NT],
+                                          f32x4 (&acc)[MT][NT]) {
     const char* t = reinterpret_cast<const char*>(lut);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-        const float sc = ((float)in.qa[nt] / 127.0f) * in.qb[nt];  // IEEE division, then fp32 multiply (:45)
+        const float sc = scs[nt];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const uint32_t wd = in.w[nt][s];
@@ -192,11 +196,12 @@ __device__ __forceinline__ void chunk_mma(const Chunk<MT, NT>& in, const float* 
 // Workgroup = WV waves owning 16 NT output columns (NT strips) of one K slice;
 // wave w takes every WV-th group of D chunks, D chunks in flight at a time; the
 // waves' partial sums are combined through LDS (fixed order, one strip at a time).
-template <int DT, int MT, int D, int WV, int NT>
+template <int DT, int MT, int D, int WV, int NT, bool VS>
 __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs A) {
     constexpr int kGemmWaves = WV;
     __shared__ __attribute__((aligned(16))) float lut[20];  // 16 codes + the last-arriver flag
     __shared__ __attribute__((aligned(16))) f32x4 red[WV][MT][64];
+    extern __shared__ __attribute__((aligned(16))) float scl[];  // VS: [16 NT rows][2 chunks_per_split blocks]
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t nl = lane & 15u, kh = lane >> 4;
@@ -214,18 +219,45 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint32_t nbs = 2u * A.chunks_per_split;  // VS: scale blocks per row in the table
     bool first = true;
     for (uint32_t g = c0 + wave * D; g < c1 || first; g += kGemmWaves * D) {
         Chunk<MT, NT> ch[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) chunk_issue<MT, NT>(A, rw, rx, g + d, g + d < c1, row, nl, kh, ch[d]);
-        if (first) {  // LUT + barrier overlap the first loads
+        for (int d = 0; d < D; ++d) chunk_issue<MT, NT, VS>(A, rw, rx, g + d, g + d < c1, row, nl, kh, ch[d]);
+        if (first) {  // LUT (+ VS: the slice's scale table) and the barrier overlap the first loads
             write_lut(lut);
+            if constexpr (VS) {
+                // the workgroup's 16 NT rows x this slice's blocks: coalesced byte / float
+                // loads (consecutive threads, consecutive blocks of a row), one IEEE
+                // division per block (:45), instead of per-lane gathers in every chunk
+                const uint32_t r0 = cg * 16u * NT, b0 = 2u * c0, nbl = 2u * (c1 - c0);
+                for (uint32_t i = threadIdx.x; i < 16u * NT * nbs; i += 64u * WV) {
+                    const uint32_t rr = i / nbs, j = i - rr * nbs;
+                    if (j < nbl) {
+                        const uint32_t r = r0 + rr, gb = b0 + j;  // no wrap inside a row (host-checked)
+                        const float q = (float)A.a1[fmodu(r * A.bpr, A.nb) + gb];
+                        scl[i] = (q / 127.0f) * A.a2[fmodu(r * A.groups, A.n2) + (gb >> 2)];
+                    }
+                }
+            }
             __syncthreads();
             first = false;
         }
 #pragma unroll
-        for (int d = 0; d < D; ++d) chunk_mma<DT, MT, NT>(ch[d], lut, acc);
+        for (int d = 0; d < D; ++d) {
+            float scs[NT];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                if constexpr (VS) {
+                    const uint32_t j = 2u * (g + d - c0) + (kh >> 1);
+                    scs[nt] = g + d < c1 ? scl[(16u * nt + nl) * nbs + j] : 0.0f;
+                } else {
+                    scs[nt] = ((float)ch[d].qa[nt] / 127.0f) * ch[d].qb[nt];  // IEEE division, fp32 multiply (:45)
+                }
+            }
+            chunk_mma<DT, MT, NT>(ch[d], lut, scs, acc);
+        }
     }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -1352,8 +1384,16 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     A.col_groups = (uint32_t)(N / (16 * nt));
     const dim3 grid(A.col_groups * ks), block(64 * cfg.waves);
     const int mt = (int)((M + 15) / 16);
-#define NF4_G(DT_, MT_, D_, W_, NT_) \
-    hipLaunchKernelGGL((nf4_gemm_smallm_kernel<DT_, MT_, D_, W_, NT_>), grid, block, 0, st, A)
+    // scale table in LDS when absmax does not wrap inside a row and the slice's table is small
+    const uint32_t scl_bytes = 16u * (uint32_t)nt * 2u * A.chunks_per_split * 4u;
+    const bool vs = scl_bytes <= 48u * 1024u && (nb % (K / 64) == 0 || nb >= N * (K / 64)) &&
+                    (n2 % (int64_t)A.groups == 0 || n2 >= N * (int64_t)A.groups);
+    const uint32_t dyn = vs ? scl_bytes : 0u;
+#define NF4_G(DT_, MT_, D_, W_, NT_)                                                                          \
+    do {                                                                                                      \
+        if (vs) hipLaunchKernelGGL((nf4_gemm_smallm_kernel<DT_, MT_, D_, W_, NT_, true>), grid, block, dyn, st, A); \
+        else hipLaunchKernelGGL((nf4_gemm_smallm_kernel<DT_, MT_, D_, W_, NT_, false>), grid, block, 0, st, A);    \
+    } while (0)
 #define NF4_N(DT_, MT_, D_, W_)                   \
     do {                                          \
         if (nt == 4) NF4_G(DT_, MT_, D_, W_, 4);  \
