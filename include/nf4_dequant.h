@@ -150,7 +150,7 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
  * 1/2/4 dividing waves) or NF4DQ_GEMM_K128 (waves 4/8, depth 1/2/4 (<= 2 when
  * M > 16), strips = 16-column strips per wave 1/2/4 (0 = 1), sharing x loads).  ksplit: K slices reduced across workgroups.
  * NF4DQ_GEMM_PERSIST: the streaming kernel's persistent form (M <= 16,
- * ksplit 1, waves / strips K parts dividing K / 256 into a multiple of depth
+ * ksplit 1..16 K slices dividing K / 256, waves / strips K parts dividing a slice into a multiple of depth
  * (2/4), x[M][K] in LDS, absmax not wrapping inside a row).
  * An invalid combination returns NF4DQ_ERR_ARG. */
 #define NF4DQ_GEMM_K128 1
@@ -173,8 +173,9 @@ int nf4_gemm_ref_cfg(const void* x, int64_t M, const uint8_t* packed, int64_t pa
  * Each weight: packed [N*K/2], its own absmax_q / absmax2 (reference wrap
  * semantics per weight), output y [M][N] (out_dtype).  Same shape rules as
  * nf4_gemm_ref for every weight (N % 64 == 0), at most NF4DQ_GEMM_GROUP_MAX
- * weights; cfg NULL = library choice for the summed N (a configuration other
- * than NF4DQ_GEMM_STREAM runs one launch per weight).  Workspace as for
+ * weights; cfg NULL = library choice for the summed N.  Every kernel runs
+ * the group as one launch (the library's persistent choice falls back to one
+ * launch per weight when absmax wraps inside a row).  Workspace as for
  * nf4_gemm_ref, sized by nf4_gemm_grouped_workspace_bytes. */
 #define NF4DQ_GEMM_GROUP_MAX 8
 typedef struct nf4_gemm_mat {

@@ -101,21 +101,33 @@ __device__ __forceinline__ void store_y(void* y, uint32_t i, float v) {
 }
 constexpr uint32_t kChunkK = 128;
 
-struct GemmArgs {
+// One weight of a 128-deep launch; weights that share x (q/k/v, gate/up) go in
+// one launch, column groups numbered over all of them.
+constexpr int kK128GroupMax = 8;
+struct K128Mat {
     const uint8_t* packed;  // [N][K/2]
     const uint8_t* a1;      // [nb]
     const float* a2;        // [n2]
-    const void* x;          // [M][K] fp16/bf16
     void* y;                // [M][N] fp16/bf16
-    float* slab;            // [ksplit][M][N] fp32 partials (ksplit > 1)
-    uint32_t* counters;     // [N / 64] split-K tickets, 0 between calls
-    uint32_t M, N, K;
-    uint32_t col_groups;    // N / 16 column strips
+    uint32_t N;
+    uint32_t cg_begin;      // first column group of this weight in the launch
+    uint32_t col_begin;     // first column in the launch (split-K slab column)
+    FastDiv nb, n2;
+};
+
+struct GemmArgs {
+    K128Mat mat[kK128GroupMax];
+    uint32_t nmat;
+    const void* x;          // [M][K] fp16/bf16
+    float* slab;            // [ksplit][M][ncols] fp32 partials (ksplit > 1)
+    uint32_t* counters;     // one split-K ticket per column group, 0 between calls
+    uint32_t M, K;
+    uint32_t ncols;         // sum of N
+    uint32_t col_groups;    // column groups (16 NT columns) over all weights
     uint32_t ksplit;
     uint32_t chunks_per_split;
     uint32_t chunks;        // K / 128
     uint32_t bpr, groups;   // K / 64, ceil(bpr / 4)
-    FastDiv nb, n2;
 };
 
 // One 128-deep K chunk of one lane: for each of the wave's NT 16-column strips,
@@ -132,9 +144,9 @@ struct Chunk {
 
 // VS: the block scales come from the workgroup's LDS table (nf4_gemm_smallm_kernel), no per-chunk gathers
 template <int MT, int NT, bool VS>
-__device__ __forceinline__ void chunk_issue(const GemmArgs& A, __amdgpu_buffer_rsrc_t rw, __amdgpu_buffer_rsrc_t rx,
-                                            uint32_t c, bool valid, uint32_t row, uint32_t nl, uint32_t kh,
-                                            Chunk<MT, NT>& in) {
+__device__ __forceinline__ void chunk_issue(const GemmArgs& A, const K128Mat& Mt, __amdgpu_buffer_rsrc_t rw,
+                                            __amdgpu_buffer_rsrc_t rx, uint32_t c, bool valid, uint32_t row,
+                                            uint32_t nl, uint32_t kh, Chunk<MT, NT>& in) {
     const uint32_t kbase = c * kChunkK + 32u * kh;
     // past the wave's last chunk: offsets beyond the buffer ranges (zeros, no traffic)
 #pragma unroll
@@ -152,8 +164,8 @@ __device__ __forceinline__ void chunk_issue(const GemmArgs& A, __amdgpu_buffer_r
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const uint32_t r = row + 16u * nt;
-            in.qa[nt] = A.a1[fmodu(r * A.bpr + b, A.nb)];             // (:173-177 wrap)
-            in.qb[nt] = A.a2[fmodu(r * A.groups + (b >> 2), A.n2)];  // (:40-41, :183-186 wrap)
+            in.qa[nt] = Mt.a1[fmodu(r * A.bpr + b, Mt.nb)];             // (:173-177 wrap)
+            in.qb[nt] = Mt.a2[fmodu(r * A.groups + (b >> 2), Mt.n2)];  // (:40-41, :183-186 wrap)
         }
     }
 }
@@ -205,13 +217,17 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t nl = lane & 15u, kh = lane >> 4;
-    const uint32_t cg = blockIdx.x % A.col_groups;   // group of NT 16-column strips
+    const uint32_t cg = blockIdx.x % A.col_groups;   // group of NT 16-column strips, launch-wide
     const uint32_t ks = blockIdx.x / A.col_groups;   // K slice
-    const uint32_t row = cg * 16u * NT + nl;         // this lane's row in strip 0; strip nt adds 16 nt
+    uint32_t mi = 0;                                 // the weight this workgroup works on (uniform scan)
+    for (uint32_t i = 1; i < A.nmat; ++i) mi = cg >= A.mat[i].cg_begin ? i : mi;
+    const K128Mat& Mt = A.mat[mi];
+    const uint32_t cgl = cg - Mt.cg_begin;           // group within the weight
+    const uint32_t row = cgl * 16u * NT + nl;        // this lane's row in strip 0; strip nt adds 16 nt
     const uint32_t c0 = ks * A.chunks_per_split;
     const uint32_t c1 = c0 + A.chunks_per_split < A.chunks ? c0 + A.chunks_per_split : A.chunks;
 
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.N * (A.K >> 1), kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
 
     f32x4 acc[MT][NT];
@@ -224,20 +240,20 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     for (uint32_t g = c0 + wave * D; g < c1 || first; g += kGemmWaves * D) {
         Chunk<MT, NT> ch[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) chunk_issue<MT, NT, VS>(A, rw, rx, g + d, g + d < c1, row, nl, kh, ch[d]);
+        for (int d = 0; d < D; ++d) chunk_issue<MT, NT, VS>(A, Mt, rw, rx, g + d, g + d < c1, row, nl, kh, ch[d]);
         if (first) {  // LUT (+ VS: the slice's scale table) and the barrier overlap the first loads
             write_lut(lut);
             if constexpr (VS) {
                 // the workgroup's 16 NT rows x this slice's blocks: coalesced byte / float
                 // loads (consecutive threads, consecutive blocks of a row), one IEEE
                 // division per block (:45), instead of per-lane gathers in every chunk
-                const uint32_t r0 = cg * 16u * NT, b0 = 2u * c0, nbl = 2u * (c1 - c0);
+                const uint32_t r0 = cgl * 16u * NT, b0 = 2u * c0, nbl = 2u * (c1 - c0);
                 for (uint32_t i = threadIdx.x; i < 16u * NT * nbs; i += 64u * WV) {
                     const uint32_t rr = i / nbs, j = i - rr * nbs;
                     if (j < nbl) {
                         const uint32_t r = r0 + rr, gb = b0 + j;  // no wrap inside a row (host-checked)
-                        const float q = (float)A.a1[fmodu(r * A.bpr, A.nb) + gb];
-                        scl[i] = (q / 127.0f) * A.a2[fmodu(r * A.groups, A.n2) + (gb >> 2)];
+                        const float q = (float)Mt.a1[fmodu(r * A.bpr, Mt.nb) + gb];
+                        scl[i] = (q / 127.0f) * Mt.a2[fmodu(r * A.groups, Mt.n2) + (gb >> 2)];
                     }
                 }
             }
@@ -286,7 +302,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const uint32_t m = 16u * mt + 4u * kh + r;
-                    if (m < A.M) store_y<DT>(A.y, m * A.N + row + 16u * nt, acc[mt][nt][r]);
+                    if (m < A.M) store_y<DT>(Mt.y, m * Mt.N + row + 16u * nt, acc[mt][nt][r]);
                 }
             }
         return;
@@ -299,7 +315,8 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     // in slice order (sc1 loads: no stale line from any L2), writes y, and
     // resets the counter to 0 for the next call.  Bitwise reproducible.
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)A.slab, 0, A.ksplit * A.M * A.N * 4u, kRsrcFlags);
+        (void*)A.slab, 0, A.ksplit * A.M * A.ncols * 4u, kRsrcFlags);
+    const uint32_t scol = Mt.col_begin + row;  // slab column of this lane (strip 0)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -307,7 +324,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint32_t m = 16u * mt + 4u * kh + r;
-                const uint32_t off = m < A.M ? ((ks * A.M + m) * A.N + row + 16u * nt) * 4u : 0xFFFFFFF0u;
+                const uint32_t off = m < A.M ? ((ks * A.M + m) * A.ncols + scol + 16u * nt) * 4u : 0xFFFFFFF0u;
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][nt][r]), rs, off, 0, kAuxSc1);
             }
         }
@@ -321,7 +338,8 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     }
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
-    splitk_reduce<DT, 16u * NT>(rs, A.ksplit, A.M, A.N, cg * 16u * NT, A.y, A.N, cg * 16u * NT, lane);
+    splitk_reduce<DT, 16u * NT>(rs, A.ksplit, A.M, A.ncols, Mt.col_begin + cgl * 16u * NT, Mt.y, Mt.N, cgl * 16u * NT,
+                                lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1325,69 +1343,49 @@ static int launch_persist(const HostMat* mats, int count, const void* x, int64_t
     return hip_rc2(hipGetLastError());
 }
 
-static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,
-                     int64_t nb, const float* absmax2, int64_t n2, void* y, int32_t dtype, int64_t N, int64_t K,
-                     void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfgp, hipStream_t st) {
-    if (dtype != NF4DQ_F16 && dtype != NF4DQ_BF16) return NF4DQ_ERR_ARG;
-    if (M < 0 || N < 0 || K < 0 || nb <= 0 || n2 <= 0) return NF4DQ_ERR_ARG;
-    if (M == 0 || N == 0) return NF4DQ_OK;
-    if (!x || !packed || !absmax_q || !absmax2 || !y) return NF4DQ_ERR_ARG;
-    if (M > NF4DQ_GEMM_MAX_M || N % 64 || K % kChunkK || packed_len != N * (K / 2)) return NF4DQ_ERR_SHAPE;
-    if ((size_t)(N / 16) * 4 > kCounterBytes) return NF4DQ_ERR_TOO_LARGE;
-    if (packed_len >= (int64_t(1) << 31) || M * K * 2 >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
-    nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, N, K);
-    if (cfg.kernel == 0) {
-        const nf4_gemm_cfg d = default_gemm_cfg(M, N, K);
-        cfg.kernel = d.kernel;
-    }
-    if (!valid_gemm_cfg(cfg, M, N, K)) return NF4DQ_ERR_ARG;
+// One launch of the 128-deep kernel over `count` weights sharing x (shapes and
+// cfg validated; workspace = counters + ksplit * M * sum(N) fp32 when ksplit > 1).
+static int launch_k128(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
+                       const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st) {
     const uint32_t ks = (uint32_t)cfg.ksplit;
-    const size_t need = workspace_for(M, N, K, cfg);
-    if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
-    if (cfg.kernel == NF4DQ_GEMM_STREAM || cfg.kernel == NF4DQ_GEMM_PERSIST) {
-        const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
-        if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
-            const int rc = launch_persist(&h, 1, x, M, K, dtype, cfg, workspace, st);
-            if ((rc != NF4DQ_ERR_ARG && rc != NF4DQ_ERR_TOO_LARGE) || cfgp) return rc;
-            // library choice that cannot run here (absmax wrapping in a row, held
-            // outputs beyond LDS): the next choice; its workspace need is covered
-            // (callers size the workspace with nf4_gemm_workspace_bytes = the max)
-            cfg = nonpersist_cfg(M, N, K);
-            const size_t w2 = workspace_for(M, N, K, cfg);
-            if (!valid_gemm_cfg(cfg, M, N, K) || (w2 && (!workspace || workspace_bytes < w2 || !aligned16(workspace))))
-                return NF4DQ_ERR_ARG;
-            if (cfg.kernel == NF4DQ_GEMM_K128)
-                return gemm_impl(x, M, packed, packed_len, absmax_q, nb, absmax2, n2, y, dtype, N, K, workspace,
-                                 workspace_bytes, &cfg, st);
-        }
-        return launch_stream(&h, 1, x, M, K, dtype, cfg, workspace, st);
-    }
+    const int nt = cfg.strips > 1 ? cfg.strips : 1;  // 16-column strips per wave
     GemmArgs A{};
-    A.packed = packed;
-    A.a1 = absmax_q;
-    A.a2 = absmax2;
+    A.nmat = (uint32_t)count;
     A.x = x;
-    A.y = y;
     A.counters = reinterpret_cast<uint32_t*>(workspace);
-    A.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + counters_bytes(N)) : nullptr;
+    A.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
     A.M = (uint32_t)M;
-    A.N = (uint32_t)N;
     A.K = (uint32_t)K;
     A.ksplit = ks;
     A.chunks = (uint32_t)(K / kChunkK);
     A.chunks_per_split = (A.chunks + ks - 1) / ks;
     A.bpr = (uint32_t)(K / 64);
     A.groups = (A.bpr + 3) / 4;
-    A.nb = make_fastdiv((uint32_t)(nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : nb));
-    A.n2 = make_fastdiv((uint32_t)(n2 > (int64_t(1) << 31) ? (int64_t(1) << 31) : n2));
-    const int nt = cfg.strips > 1 ? cfg.strips : 1;  // 16-column strips per wave
-    A.col_groups = (uint32_t)(N / (16 * nt));
+    // scale table in LDS when absmax does not wrap inside a row (any weight) and the slice's table is small
+    const uint32_t scl_bytes = 16u * (uint32_t)nt * 2u * A.chunks_per_split * 4u;
+    bool vs = scl_bytes <= 48u * 1024u;
+    uint32_t cgs = 0, cols = 0;
+    for (int i = 0; i < count; ++i) {
+        const HostMat& h = mats[i];
+        K128Mat& m = A.mat[i];
+        m.packed = h.packed;
+        m.a1 = h.a1;
+        m.a2 = h.a2;
+        m.y = h.y;
+        m.N = (uint32_t)h.N;
+        m.cg_begin = cgs;
+        m.col_begin = cols;
+        m.nb = make_fastdiv((uint32_t)(h.nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : h.nb));
+        m.n2 = make_fastdiv((uint32_t)(h.n2 > (int64_t(1) << 31) ? (int64_t(1) << 31) : h.n2));
+        cgs += (uint32_t)(h.N / (16 * nt));
+        cols += (uint32_t)h.N;
+        vs = vs && (h.nb % (K / 64) == 0 || h.nb >= h.N * (K / 64)) &&
+             (h.n2 % (int64_t)A.groups == 0 || h.n2 >= h.N * (int64_t)A.groups);
+    }
+    A.col_groups = cgs;
+    A.ncols = cols;
     const dim3 grid(A.col_groups * ks), block(64 * cfg.waves);
     const int mt = (int)((M + 15) / 16);
-    // scale table in LDS when absmax does not wrap inside a row and the slice's table is small
-    const uint32_t scl_bytes = 16u * (uint32_t)nt * 2u * A.chunks_per_split * 4u;
-    const bool vs = scl_bytes <= 48u * 1024u && (nb % (K / 64) == 0 || nb >= N * (K / 64)) &&
-                    (n2 % (int64_t)A.groups == 0 || n2 >= N * (int64_t)A.groups);
     const uint32_t dyn = vs ? scl_bytes : 0u;
 #define NF4_G(DT_, MT_, D_, W_, NT_)                                                                          \
     do {                                                                                                      \
@@ -1425,8 +1423,49 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     return hip_rc2(hipGetLastError());
 }
 
-// Weights that share x, one launch when the streaming kernel applies; otherwise
-// one nf4_gemm_ref-equivalent launch per weight (same workspace, sequential on st).
+static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,
+                     int64_t nb, const float* absmax2, int64_t n2, void* y, int32_t dtype, int64_t N, int64_t K,
+                     void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfgp, hipStream_t st) {
+    if (dtype != NF4DQ_F16 && dtype != NF4DQ_BF16) return NF4DQ_ERR_ARG;
+    if (M < 0 || N < 0 || K < 0 || nb <= 0 || n2 <= 0) return NF4DQ_ERR_ARG;
+    if (M == 0 || N == 0) return NF4DQ_OK;
+    if (!x || !packed || !absmax_q || !absmax2 || !y) return NF4DQ_ERR_ARG;
+    if (M > NF4DQ_GEMM_MAX_M || N % 64 || K % kChunkK || packed_len != N * (K / 2)) return NF4DQ_ERR_SHAPE;
+    if ((size_t)(N / 16) * 4 > kCounterBytes) return NF4DQ_ERR_TOO_LARGE;
+    if (packed_len >= (int64_t(1) << 31) || M * K * 2 >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
+    nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, N, K);
+    if (cfg.kernel == 0) {
+        const nf4_gemm_cfg d = default_gemm_cfg(M, N, K);
+        cfg.kernel = d.kernel;
+    }
+    if (!valid_gemm_cfg(cfg, M, N, K)) return NF4DQ_ERR_ARG;
+    const size_t need = workspace_for(M, N, K, cfg);
+    if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
+    if (cfg.kernel == NF4DQ_GEMM_STREAM || cfg.kernel == NF4DQ_GEMM_PERSIST) {
+        const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
+        if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
+            const int rc = launch_persist(&h, 1, x, M, K, dtype, cfg, workspace, st);
+            if ((rc != NF4DQ_ERR_ARG && rc != NF4DQ_ERR_TOO_LARGE) || cfgp) return rc;
+            // library choice that cannot run here (absmax wrapping in a row, held
+            // outputs beyond LDS): the next choice; its workspace need is covered
+            // (callers size the workspace with nf4_gemm_workspace_bytes = the max)
+            cfg = nonpersist_cfg(M, N, K);
+            const size_t w2 = workspace_for(M, N, K, cfg);
+            if (!valid_gemm_cfg(cfg, M, N, K) || (w2 && (!workspace || workspace_bytes < w2 || !aligned16(workspace))))
+                return NF4DQ_ERR_ARG;
+            if (cfg.kernel == NF4DQ_GEMM_K128)
+                return gemm_impl(x, M, packed, packed_len, absmax_q, nb, absmax2, n2, y, dtype, N, K, workspace,
+                                 workspace_bytes, &cfg, st);
+        }
+        return launch_stream(&h, 1, x, M, K, dtype, cfg, workspace, st);
+    }
+    const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
+    return launch_k128(&h, 1, x, M, K, dtype, cfg, workspace, st);
+}
+
+// Weights that share x, one launch of whichever kernel cfg names (workgroups
+// numbered over all the weights' strips / column groups); the library's
+// persistent choice, when it cannot run, falls back to per-weight launches.
 static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm_mat* mats, int32_t count,
                              int32_t dtype, void* workspace, size_t workspace_bytes, const nf4_gemm_cfg* cfgp,
                              hipStream_t st) {
@@ -1447,17 +1486,12 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
     if ((size_t)(ntot / 16) * 4 > kCounterBytes) return NF4DQ_ERR_TOO_LARGE;
     nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, ntot, K);
     if (cfg.kernel == 0) cfg.kernel = default_gemm_cfg(M, ntot, K).kernel;
-    if (cfg.kernel != NF4DQ_GEMM_STREAM && cfg.kernel != NF4DQ_GEMM_PERSIST) {
-        for (int i = 0; i < count; ++i) {
-            const nf4_gemm_mat& m = mats[i];
-            const int rc = gemm_impl(x, M, m.packed, m.packed_len, m.absmax_q, m.nb, m.absmax2, m.n2, m.y, dtype, m.N,
-                                     K, workspace, workspace_bytes, cfgp, st);
-            if (rc) return rc;
-        }
-        return NF4DQ_OK;
-    }
+    static_assert(kK128GroupMax == NF4DQ_GEMM_GROUP_MAX && kGroupMax == NF4DQ_GEMM_GROUP_MAX, "group sizes");
     for (int i = 0; i < count; ++i) {
-        if (mats[i].N == 0) return NF4DQ_ERR_SHAPE;  // an empty weight cannot own strip groups
+        // an empty weight cannot own strip groups (the 128-deep kernel numbers
+        // column groups per weight: an empty one simply owns none)
+        if (mats[i].N == 0 && cfg.kernel != NF4DQ_GEMM_K128) return NF4DQ_ERR_SHAPE;
+        if (mats[i].N == 0) continue;
         if (!valid_gemm_cfg(cfg, M, mats[i].N, K)) return NF4DQ_ERR_ARG;
         if (mats[i].packed_len >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
     }
@@ -1468,6 +1502,7 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
     for (int i = 0; i < count; ++i)
         h[i] = HostMat{mats[i].packed, mats[i].packed_len, mats[i].absmax_q, mats[i].nb, mats[i].absmax2,
                        mats[i].n2, mats[i].y, mats[i].N};
+    if (cfg.kernel == NF4DQ_GEMM_K128) return launch_k128(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
         const int rc = launch_persist(h, count, x, M, K, dtype, cfg, workspace, st);
         if ((rc != NF4DQ_ERR_ARG && rc != NF4DQ_ERR_TOO_LARGE) || cfgp) return rc;
@@ -1495,17 +1530,12 @@ static size_t grouped_workspace(int64_t M, int64_t K, const nf4_gemm_mat* mats, 
     if (ntot <= 0) return 0;
     nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, ntot, K);
     if (cfg.kernel == 0) cfg.kernel = default_gemm_cfg(M, ntot, K).kernel;
-    size_t w = 0;
-    if (cfg.kernel == NF4DQ_GEMM_STREAM || cfg.kernel == NF4DQ_GEMM_PERSIST) {
-        w = cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
-        if (cfgp || cfg.kernel == NF4DQ_GEMM_STREAM) return w;
-    }
-    // per-weight launches (the 128-deep kernel, or the library's fallback from
-    // the persistent kernel): the largest of their needs
+    size_t w = cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
+    if (cfgp || cfg.kernel != NF4DQ_GEMM_PERSIST) return w;
+    // the library's persistent choice may fall back to per-weight launches
+    // (gemm_grouped_impl): the largest of their needs as well
     for (int i = 0; i < count; ++i) {
-        const nf4_gemm_cfg c = cfgp ? *cfgp : (cfg.kernel == NF4DQ_GEMM_PERSIST ? nonpersist_cfg(M, mats[i].N, K)
-                                                                                : default_gemm_cfg(M, mats[i].N, K));
-        const size_t wi = workspace_for(M, mats[i].N, K, c);
+        const size_t wi = workspace_for(M, mats[i].N, K, nonpersist_cfg(M, mats[i].N, K));
         w = wi > w ? wi : w;
     }
     (void)nmax;

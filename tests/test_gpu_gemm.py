@@ -225,7 +225,9 @@ def test_invalid_decompositions_rejected(gpu):
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("M,K,Ns", [(1, 4096, (4096, 1024, 1024)), (4, 2048, (512, 1536)),
-                                    (3, 1280, (64, 128, 192, 256, 320, 384, 448, 512)), (16, 512, (1024, 64))])
+                                    (3, 1280, (64, 128, 192, 256, 320, 384, 448, 512)), (16, 512, (1024, 64)),
+                                    (24, 1280, (64, 128, 192, 256, 320)), (32, 4096, (4096, 1024, 1024)),
+                                    (20, 384, (192, 64))])
 def test_grouped_gemm_vs_float64_oracle(coracle, gpu, dt, M, K, Ns):
     """Weights sharing x in one launch: each output against its own float64 oracle."""
     from nf4_triton_dequantization_amd import nf4_linear_grouped
@@ -305,6 +307,54 @@ def test_persistent_grouped_gemm(coracle, gpu, cfg):
     xt, xb = _x_bits(M, K, "bf16", seed=4)
     x = xt.to(gpu)
     c = _lib.GemmCfg(_lib.GEMM_PERSIST, waves, depth, ks, strips)
+    wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, mats, len(Ns), ctypes.byref(c))
+    assert (wsz > 0) == (ks > 1)
+    ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=gpu)
+    for _ in range(2):  # the second call reuses the tickets the first left at 0
+        for y in ys:
+            y.fill_(float("nan"))
+        rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, mats, len(Ns), _lib.BF16, ws.data_ptr() if wsz else None,
+                                    wsz, ctypes.byref(c), torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+        for y, W in zip(ys, Ws):
+            _check(y, xb, W, "bf16")
+    if ks > 1:
+        assert int(ws[:65536].view(torch.int32).abs().sum()) == 0  # tickets back at 0
+
+
+@pytest.mark.parametrize("cfg", [(4, 2, 1, 1, 3), (8, 2, 2, 1, 16), (8, 2, 4, 2, 20), (4, 1, 2, 3, 32),
+                                 (8, 4, 1, 4, 8), (8, 1, 4, 8, 32)])
+@pytest.mark.parametrize("wrap", [False, True])
+def test_k128_grouped_gemm(coracle, gpu, cfg, wrap):
+    """The 128-deep kernel over ONE grouped launch (column groups numbered over all
+    weights, K slices summed per group); `wrap` adds a weight whose absmax wraps inside
+    a row, which turns the LDS scale table off for the whole launch."""
+    import ctypes
+
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    waves, depth, strips, ks, M = cfg
+    K = 2048
+    Ns = (1024, 256, 512) + ((128,) if wrap else ())
+    mats = (_lib.GemmMat * len(Ns))()
+    ys, keep, Ws = [], [], []
+    for i, N in enumerate(Ns):
+        if wrap and i == 3:
+            packed, a1, a2 = O.golden_case_inputs(N, K, 5, {"nb": 37, "n2": 5})[:3]
+        else:
+            packed, a1, a2 = O.make_inputs(N, K, seed=3 * N + i, a2_kind="normal")
+        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16))
+        t = [torch.from_numpy(v).to(gpu) for v in (packed, a1, a2)]
+        keep.append(t)
+        y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+        ys.append(y)
+        mats[i] = _lib.GemmMat(t[0].data_ptr(), t[0].numel(), t[1].data_ptr(), t[1].numel(), t[2].data_ptr(),
+                               t[2].numel(), y.data_ptr(), N)
+    xt, xb = _x_bits(M, K, "bf16", seed=M + 40)
+    x = xt.to(gpu)
+    c = _lib.GemmCfg(_lib.GEMM_K128, waves, depth, ks, strips)
     wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, mats, len(Ns), ctypes.byref(c))
     assert (wsz > 0) == (ks > 1)
     ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=gpu)
