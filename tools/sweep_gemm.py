@@ -51,12 +51,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", default="1,16,32")
     ap.add_argument("--budget-mb", type=int, default=768, help="packed weight bytes per shape")
+    ap.add_argument("--shapes", default="", help="N,K;N,K;... (default: the Llama-3-8B list)")
+    ap.add_argument("--kernels", default="1,2,3", help="kernel ids to sweep (1 K128, 2 stream, 3 persist)")
     args = ap.parse_args()
+    shapes = [tuple(int(v) for v in s.split(",")) for s in args.shapes.split(";")] if args.shapes else SHAPES
+    kern = {int(v) for v in args.kernels.split(",")}
     dev = torch.device("cuda", 0)
     L = _lib.lib()
     gen = torch.Generator(device=dev)
     gen.manual_seed(0)
-    for (n, k) in SHAPES:
+    for (n, k) in shapes:
         copies = max(8, args.budget_mb * (1 << 20) // (n * k // 2))
         nb = n * k // 64
         ws = [(torch.randint(0, 256, (n * k // 2,), dtype=torch.uint8, device=dev, generator=gen),
@@ -83,6 +87,7 @@ def main():
                     for strips in (1, 2, 4):  # K128: strips per wave
                         for ks in (1, 2, 4, 8):
                             cfgs.append(_lib.GemmCfg(_lib.GEMM_K128, waves, depth, ks, strips))
+            cfgs = [c for c in cfgs if c.kernel in kern]
             for cfg in cfgs:
                 wsz = L.nf4_gemm_workspace_bytes_cfg(M, n, k, ctypes.byref(cfg))
                 work = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=dev)
