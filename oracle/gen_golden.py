@@ -67,6 +67,15 @@ BIG_CASES = [
     ("C2_4096x4096_bf16", 4096, 4096, "bf16", 3409, {}),
     ("c64x11008_bf16", 64, 11008, "bf16", 3408, {}),
     ("c1024x4096_f16_neg", 1024, 4096, "f16", 3410, {"a2_kind": "normal"}),
+    # BASELINE configs at full size (round 2): C4's fp16 leg, C5's per-GPU unit and
+    # every distinct C3 shape (Llama-3-8B 1024/4096/14336 and Llama-2-7B 11008)
+    ("C4_4096x4096_f16", 4096, 4096, "f16", 3409, {}),
+    ("C5_8192x8192_bf16", 8192, 8192, "bf16", 3411, {}),
+    ("C3_1024x4096_bf16", 1024, 4096, "bf16", 3420, {}),
+    ("C3_14336x4096_bf16", 14336, 4096, "bf16", 3421, {}),
+    ("C3_4096x14336_bf16", 4096, 14336, "bf16", 3422, {}),
+    ("C3b_11008x4096_bf16", 11008, 4096, "bf16", 3423, {}),
+    ("C3b_4096x11008_bf16", 4096, 11008, "bf16", 3424, {}),
 ]
 
 
@@ -133,14 +142,24 @@ print('JSON' + json.dumps(res))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--triton-interp", action="store_true")
+    ap.add_argument("--only", default="", help="comma-separated case names: (re)generate just these and keep "
+                                               "every other entry of the existing manifest")
     args = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
+    only = {x for x in args.only.split(",") if x}
     manifest = {"generator": "oracle/gen_golden.py",
                 "reference": "nf4_triton_dequantization/kernel_optimized.py:208-314 (_aggressive_pytorch_t4)",
                 "cases": {}}
     samples = {}
+    if only:
+        with open(os.path.join(GOLDEN, "manifest.json")) as f:
+            manifest = json.load(f)
+        with np.load(os.path.join(GOLDEN, "big_samples.npz"), allow_pickle=False) as z:
+            samples = {k: z[k] for k in z.files}
     for big, cases in ((False, SMALL_CASES), (True, BIG_CASES)):
         for name, m, n, dt, seed, ov in cases:
+            if only and name not in only:
+                continue
             packed, a1, a2, single = case_inputs(m, n, seed, ov)
             mod = torch_module(packed, a1, a2, single, m, n, dt, ov)
             out = run_reference(mod)

@@ -16,9 +16,8 @@ reference fallback ``_aggressive_pytorch_t4``,
 /root/reference/nf4_triton_dequantization/kernel_optimized.py:208-314, via
 ``oracle/gen_golden.py``).
 
-Also here: ``splitmix64_bytes`` -- the deterministic input generator shared by the
-fixture script, the tests and the bench, so the GPU box regenerates identical
-inputs without depending on torch's RNG.
+The deterministic input generator (``splitmix64_bytes`` & co.) lives in
+``workloads.py`` at the repo root and is re-exported here.
 """
 from __future__ import annotations
 
@@ -43,61 +42,15 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 # ----------------------------------------------------------------------------
-# deterministic inputs
+# deterministic inputs: the shared generator lives in /workloads.py (the bench and
+# tools use it too); re-exported here for the fixture script and the tests
 # ----------------------------------------------------------------------------
-_GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+import sys as _sys  # noqa: E402
 
-
-def splitmix64(seed: int, count: int, stream: int = 0) -> np.ndarray:
-    """``count`` splitmix64 outputs for (seed, stream): a stateless counter hash."""
-    with np.errstate(over="ignore"):
-        base = np.uint64((seed * 0x100000001B3 + stream * 0x5851F42D4C957F2D) & 0xFFFFFFFFFFFFFFFF)
-        x = base + (np.arange(1, count + 1, dtype=np.uint64) * _GOLDEN)
-        z = x
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        return z ^ (z >> np.uint64(31))
-
-
-def splitmix64_bytes(seed: int, nbytes: int, stream: int = 0) -> np.ndarray:
-    words = splitmix64(seed, (nbytes + 7) // 8, stream)
-    return words.view(np.uint8)[:nbytes].copy()
-
-
-def uniform_f32(seed: int, count: int, lo: float, hi: float, stream: int = 0) -> np.ndarray:
-    """Uniform fp32 in [lo, hi) from the top 24 bits of splitmix64."""
-    u = (splitmix64(seed, count, stream) >> np.uint64(40)).astype(np.float64) / float(1 << 24)
-    return (lo + (hi - lo) * u).astype(np.float32)
-
-
-def normal_f32(seed: int, count: int, stream: int = 0) -> np.ndarray:
-    """Box-Muller N(0,1) in fp32 (includes negatives)."""
-    w = splitmix64(seed, count, stream)
-    u1 = ((w >> np.uint64(40)).astype(np.float64) + 0.5) / float(1 << 24)
-    u2 = ((w & np.uint64(0xFFFFFF)).astype(np.float64) + 0.5) / float(1 << 24)
-    return (np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)).astype(np.float32)
-
-
-def make_inputs(m: int, n: int, seed: int, *, nb: int | None = None, n2: int | None = None,
-                a2_kind: str = "uniform"):
-    """Synthetic bnb-layout inputs: packed bytes, A1 u8, A2 fp32.
-
-    Default counts are real-bnb counts: nb = ceil(m*n/64), n2 = ceil(nb/256).
-    """
-    numel = m * n
-    if nb is None:
-        nb = (numel + 63) // 64
-    if n2 is None:
-        n2 = (nb + 255) // 256
-    packed = splitmix64_bytes(seed, numel // 2, stream=1)
-    a1 = splitmix64_bytes(seed, nb, stream=2)
-    if a2_kind == "uniform":
-        a2 = uniform_f32(seed, n2, 1e-3, 1e-2, stream=3)
-    elif a2_kind == "normal":
-        a2 = normal_f32(seed, n2, stream=3)
-    else:
-        raise ValueError(a2_kind)
-    return packed, a1, a2
+_REPO = os.path.dirname(_HERE)
+if _REPO not in _sys.path:
+    _sys.path.insert(0, _REPO)
+from workloads import make_inputs, normal_f32, splitmix64, splitmix64_bytes, uniform_f32  # noqa: E402,F401
 
 
 def golden_case_inputs(m: int, n: int, seed: int, ov: dict):

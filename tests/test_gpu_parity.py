@@ -44,8 +44,12 @@ def test_golden_small_cases_bit_exact(manifest, gpu):
             assert max_abs_diff(got, z["out_bits"], dt) <= TOL_F16_MAX_ABS
 
 
+# every full-size case of the manifest: C1, C2, C4's fp16 leg, C5's per-GPU 8192^2
+# unit and each distinct C3 shape (Llama-3-8B and Llama-2-7B linears)
 @pytest.mark.parametrize("name", ["C1_1024x1024_f16", "C2_4096x4096_bf16", "c64x11008_bf16",
-                                  "c1024x4096_f16_neg"])
+                                  "c1024x4096_f16_neg", "C4_4096x4096_f16", "C5_8192x8192_bf16",
+                                  "C3_1024x4096_bf16", "C3_14336x4096_bf16", "C3_4096x14336_bf16",
+                                  "C3b_11008x4096_bf16", "C3b_4096x11008_bf16"])
 def test_full_size_matches_reference_digest(manifest, gpu, name):
     e = manifest["cases"][name]
     m, n, dt = e["m"], e["n"], e["dtype"]

@@ -62,9 +62,18 @@ def test_fixture_inputs_regenerate(manifest):
             assert np.array_equal(single, z["absmax_f32"]), name
 
 
-@pytest.mark.parametrize("name", ["C1_1024x1024_f16", "C2_4096x4096_bf16", "c64x11008_bf16",
-                                  "c1024x4096_f16_neg"])
+BIG_NAMES = ["C1_1024x1024_f16", "C2_4096x4096_bf16", "c64x11008_bf16", "c1024x4096_f16_neg",
+             "C4_4096x4096_f16", "C5_8192x8192_bf16", "C3_1024x4096_bf16", "C3_14336x4096_bf16",
+             "C3_4096x14336_bf16", "C3b_11008x4096_bf16", "C3b_4096x11008_bf16"]
+
+
+def test_every_big_case_is_checked(manifest):
+    assert set(BIG_NAMES) == {k for k, _ in _big(manifest)}
+
+
+@pytest.mark.parametrize("name", BIG_NAMES)
 def test_c_oracle_matches_reference_digest_full_size(manifest, coracle, name):
+    coracle.set_threads(8)
     e = manifest["cases"][name]
     p, a1, a2, _ = O.golden_case_inputs(e["m"], e["n"], e["seed"], e["overrides"])
     got = coracle.dequant_ref(p, a1, a2, e["m"], e["n"], DT_CODE[e["dtype"]])
