@@ -15,6 +15,9 @@
  *   nf4_dequant_single <- the non-uint8 absmax branch :166-167 -> :273-274
  *   nf4_dequant_ref_batched <- benchmark.py:68-84 (several Linear4bit weights
  *                         per step) folded into one launch
+ *   nf4_dequant_ref_cpu / nf4_dequant_single_cpu <- _aggressive_pytorch_t4
+ *                         :208-314, the reference's CPU path (HOST pointers,
+ *                         synchronous, `threads` worker threads)
  *   nf4_dequant_bnb / nf4_dequant_bnb_single <- bitsandbytes dequantize_4bit
  *                         semantics; the reference
  *                         never implements these, they are parity-unpinned.
@@ -60,6 +63,22 @@ int nf4_dequant_single(const uint8_t* packed, int64_t packed_len,
                        const float* absmax, int64_t absmax_len,
                        void* out, int32_t out_dtype, int64_t m, int64_t n,
                        void* hip_stream);
+
+/* Host-CPU forms of nf4_dequant_ref / nf4_dequant_single:
+ * same arguments, same semantics bit for bit, same error codes, but every
+ * pointer is a HOST pointer and the call is synchronous; `threads` worker
+ * threads split the rows (<= 0 = all hardware threads).  AVX2 table lookups
+ * when the CPU has AVX2, a scalar loop otherwise (same results).  Replaces the
+ * reference's CPU fallback _aggressive_pytorch_t4 (kernel_optimized.py:208-314). */
+int nf4_dequant_ref_cpu(const uint8_t* packed, int64_t packed_len,
+                        const uint8_t* absmax_q, int64_t nb,
+                        const float* absmax2, int64_t n2,
+                        void* out, int32_t out_dtype, int64_t m, int64_t n,
+                        int32_t threads);
+int nf4_dequant_single_cpu(const uint8_t* packed, int64_t packed_len,
+                           const float* absmax, int64_t absmax_len,
+                           void* out, int32_t out_dtype, int64_t m, int64_t n,
+                           int32_t threads);
 
 /* One matrix of a batched call (host memory; copied into kernel arguments). */
 typedef struct nf4_matrix_desc {

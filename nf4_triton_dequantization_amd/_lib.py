@@ -87,6 +87,8 @@ _P, _I64, _I32, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_f
 SIGNATURES = {
     "nf4_dequant_ref": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I32, _I64, _I64, _P]),
     "nf4_dequant_single": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I32, _I64, _I64, _P]),
+    "nf4_dequant_ref_cpu": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I32, _I64, _I64, _I32]),
+    "nf4_dequant_single_cpu": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I32, _I64, _I64, _I32]),
     "nf4_dequant_ref_batched": (ctypes.c_int, [ctypes.POINTER(MatrixDesc), _I32, _I32, _P]),
     "nf4_dequant_bnb": (ctypes.c_int, [_P, _P, _I64, _P, _P, _I64, _F, _P, _I32, _I64, _I32, _I32, _P]),
     "nf4_dequant_bnb_single": (ctypes.c_int, [_P, _P, _I64, _P, _I32, _I64, _I32, _P]),

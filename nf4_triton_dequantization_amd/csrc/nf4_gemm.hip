@@ -224,7 +224,11 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     const K128Mat& Mt = A.mat[mi];
     const uint32_t cgl = cg - Mt.cg_begin;           // group within the weight
     const uint32_t row = cgl * 16u * NT + nl;        // this lane's row in strip 0; strip nt adds 16 nt
-    const uint32_t c0 = ks * A.chunks_per_split;
+    // a slice may start past the end (e.g. K = 4096, ksplit = 12: ceil(32/12) = 3
+    // chunks per slice, slice 11 starts at 33): clamp so it is empty (c1 == c0),
+    // never a wrapped block count
+    const uint32_t c0s = ks * A.chunks_per_split;
+    const uint32_t c0 = c0s < A.chunks ? c0s : A.chunks;
     const uint32_t c1 = c0 + A.chunks_per_split < A.chunks ? c0 + A.chunks_per_split : A.chunks;
 
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);

@@ -29,6 +29,7 @@ consumer ``x @ W.t()`` fused: ``nf4_linear`` / ``nf4_linear_grouped``.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Iterable, List, Optional, Sequence
 
 import torch
@@ -38,11 +39,37 @@ from . import _lib
 _DTYPE_CODE = {torch.float16: _lib.F16, torch.bfloat16: _lib.BF16, torch.float32: _lib.F32}
 
 
+BACKEND_ENV = "NF4_BACKEND"
+THREADS_ENV = "NF4_CPU_THREADS"
+
+
+def backend() -> str:
+    """Where host (CPU) tensors go: ``NF4_BACKEND`` = ``hip`` (default) or ``cpu``.
+
+    ``hip`` keeps the reference's behaviour: a weight on the host raises
+    (the reference hands it to Triton, which has no CPU driver).  ``cpu`` runs
+    host tensors through the library's own host path (``nf4_dequant_ref_cpu``,
+    SURVEY §8b), bit-identical to the HIP kernels and to the reference
+    fallback.  Device tensors always run on their device.  Read on every call.
+    """
+    b = os.environ.get(BACKEND_ENV, "hip").strip().lower() or "hip"
+    if b not in ("hip", "cpu"):
+        raise ValueError(f"{BACKEND_ENV}={b!r}: expected 'hip' or 'cpu'")
+    return b
+
+
+def cpu_threads() -> int:
+    """Worker threads of the host path: ``NF4_CPU_THREADS``, else torch's intra-op thread count."""
+    v = os.environ.get(THREADS_ENV, "")
+    return int(v) if v.strip() else torch.get_num_threads()
+
+
 def _dtype_code(dtype: torch.dtype) -> int:
     try:
         return _DTYPE_CODE[dtype]
     except KeyError:
-        raise TypeError(f"unsupported quant_state.dtype {dtype}; expected float16, bfloat16 or float32") from None
+        raise TypeError(f"unsupported quant_state.dtype {dtype}; expected float16, bfloat16, float32 "
+                        f"or float64") from None
 
 
 def _require_device(t: torch.Tensor) -> None:
@@ -132,28 +159,95 @@ def dequantize_nf4_into(qweight: torch.Tensor, absmax: torch.Tensor, absmax32: t
     return out
 
 
+def _launch_cpu(qweight, absmax, absmax32, out, m, n, code) -> None:
+    """NF4_BACKEND=cpu: the same casts and checks, then the library's host path
+    (``nf4_dequant_ref_cpu`` / ``nf4_dequant_single_cpu``, synchronous)."""
+    for t in (absmax, absmax32) if absmax.dtype == torch.uint8 else (absmax,):
+        if t.device.type != "cpu":
+            raise RuntimeError(f"NF4 quant state tensor on '{t.device}', packed weight on the host: "
+                               f"all of them must be on the same device")
+    if qweight.dtype != torch.uint8:
+        qweight = qweight.to(torch.uint8)  # value cast, as :162-163
+    qweight, qp, qn = _flat_ptr(qweight)
+    L = _lib.lib()
+    threads = cpu_threads()
+    if absmax.dtype == torch.uint8:
+        if absmax32.dtype != torch.float32:
+            absmax32 = absmax32.to(torch.float32)  # :182
+        absmax, ap, an = _flat_ptr(absmax)
+        absmax32, bp, bn = _flat_ptr(absmax32)
+        if an == 0 or bn == 0:
+            raise ZeroDivisionError("integer division or modulo by zero (empty absmax)")
+        rc = L.nf4_dequant_ref_cpu(qp, qn, ap, an, bp, bn, out.data_ptr(), code, m, n, threads)
+    else:
+        if absmax.dtype != torch.float32:
+            absmax = absmax.to(torch.float32)
+        absmax, ap, an = _flat_ptr(absmax)
+        rc = L.nf4_dequant_single_cpu(qp, qn, ap, an, out.data_ptr(), code, m, n, threads)
+    if rc:
+        _lib.check(rc, "nf4 dequantize (cpu)")
+
+
+_REF = None  # bound nf4_dequant_ref (fast path: one attribute lookup less per call)
+_raw_stream = torch._C._cuda_getCurrentRawStream  # device index -> hipStream_t of the current stream
+_U8, _F32 = torch.uint8, torch.float32
+
+
+def _dequantize(qweight, absmax, absmax32, dtype, m, n) -> torch.Tensor:
+    if dtype == torch.float64:
+        # the reference computes in fp32 and casts on the store (:109-110, :310):
+        # fp64 output = the fp32 product, widened exactly
+        return _dequantize(qweight, absmax, absmax32, torch.float32, m, n).to(torch.float64)
+    code = _dtype_code(dtype)  # raise before allocating
+    dev = qweight.device
+    if dev.type != "cuda":
+        if dev.type != "cpu" or backend() != "cpu":
+            _require_device(qweight)
+        out = torch.empty((m, n), dtype=dtype)
+        if m and n:
+            _launch_cpu(qweight, absmax, absmax32, out, m, n, code)
+        return out
+    out = torch.empty((m, n), dtype=dtype, device=dev)
+    if m == 0 or n == 0:
+        return out
+    idx = dev.index
+    if idx == torch.cuda.current_device():
+        # fast path: inputs already in the kernel's types, contiguous, on this device
+        if (qweight.dtype == _U8 and absmax.dtype == _U8 and absmax32.dtype == _F32 and qweight.is_contiguous()
+                and absmax.is_contiguous() and absmax32.is_contiguous() and absmax.device == dev
+                and absmax32.device == dev):
+            nb = absmax.numel()
+            n2 = absmax32.numel()
+            if nb and n2:
+                global _REF
+                if _REF is None:
+                    _REF = _lib.lib().nf4_dequant_ref
+                rc = _REF(qweight.data_ptr(), qweight.numel(), absmax.data_ptr(), nb, absmax32.data_ptr(), n2,
+                          out.data_ptr(), code, m, n, _raw_stream(idx))
+                if rc:
+                    _lib.check(rc, "nf4 dequantize")
+                return out
+        _launch(qweight, absmax, absmax32, out, m, n, code, _raw_stream(idx))
+    else:
+        with torch.cuda.device(dev):
+            _launch(qweight, absmax, absmax32, out, m, n, code, torch.cuda.current_stream().cuda_stream)
+    return out
+
+
 def triton_dequantize_nf4(module) -> torch.Tensor:
     """Dequantize a bitsandbytes-layout NF4 ``Linear4bit`` weight to ``[out_features, in_features]``.
 
     Drop-in for ``nf4_triton_dequantization.triton_dequantize_nf4``
     (kernel_optimized.py:113).  Returns a new contiguous tensor of
-    ``quant_state.dtype`` on the weight's device.
+    ``quant_state.dtype`` on the weight's device.  Host tensors raise (as the
+    reference's Triton path does) unless ``NF4_BACKEND=cpu`` selects the
+    library's host path.
     """
-    qweight, absmax, absmax32, dtype, m, n = _prepare(module)
-    dev = qweight.device
-    if dev.type != "cuda":
-        _require_device(qweight)
-    code = _dtype_code(dtype)  # raise before allocating
-    out = torch.empty((m, n), dtype=dtype, device=dev)
-    if m == 0 or n == 0:
-        return out
-    idx = dev.index
-    if idx is None or idx == torch.cuda.current_device():
-        _launch(qweight, absmax, absmax32, out, m, n, code, torch.cuda.current_stream().cuda_stream)
-    else:
-        with torch.cuda.device(dev):
-            _launch(qweight, absmax, absmax32, out, m, n, code, torch.cuda.current_stream().cuda_stream)
-    return out
+    weight = module.weight
+    quant_state = weight.quant_state
+    absmax32 = quant_state.state2.absmax  # AttributeError when state2 is None, as :151
+    return _dequantize(weight.data, quant_state.absmax, absmax32, quant_state.dtype, int(module.out_features),
+                       int(module.in_features))
 
 
 def reset_triton_dequantize_state() -> None:
@@ -174,8 +268,9 @@ def dequantize_nf4_many(modules: Iterable) -> List[torch.Tensor]:
     keep = []  # tensors referenced by descriptors must outlive the launch
     for i, mod in enumerate(modules):
         qweight, absmax, absmax32, dtype, m, n = _prepare(mod)
-        _require_device(qweight)
-        if absmax.dtype != torch.uint8:
+        if qweight.device.type != "cuda" or absmax.dtype != torch.uint8 or dtype not in _DTYPE_CODE:
+            # host tensors (NF4_BACKEND=cpu, or the reference's error), single-quant
+            # absmax, fp64 output: one call each
             outs[i] = triton_dequantize_nf4(mod)
             continue
         code = _dtype_code(dtype)
@@ -289,14 +384,16 @@ def nf4_linear(x: torch.Tensor, module, bias: Optional[torch.Tensor] = None) -> 
     inputs already are.
     """
     qweight, absmax, absmax32, dtype, m, n = _prepare(module)
-    _require_device(qweight)
+    if qweight.device.type != "cuda" and backend() != "cpu":
+        _require_device(qweight)
     _same_device(x, qweight)
     N, K = m, n
     if x.shape[-1] != K:
         raise RuntimeError(f"nf4_linear: x has {x.shape[-1]} features, weight expects {K}")
     lead = x.shape[:-1]
     M = x.numel() // K if K else 0
-    fused = (dtype in (torch.float16, torch.bfloat16) and absmax.dtype == torch.uint8 and 0 < M <= _lib.GEMM_MAX_M
+    fused = (qweight.device.type == "cuda" and dtype in (torch.float16, torch.bfloat16)
+             and absmax.dtype == torch.uint8 and 0 < M <= _lib.GEMM_MAX_M
              and N % 64 == 0 and K % 128 == 0 and qweight.numel() * qweight.element_size() == N * K // 2
              and qweight.dtype == torch.uint8)
     if not fused:
@@ -369,13 +466,15 @@ def nf4_linear_grouped(x: torch.Tensor, modules: Sequence, biases: Optional[Sequ
     for i, (q, a1, a2, _dt, m, _n) in enumerate(preps):
         _on_device(dev, a1, a2)
         y = torch.empty((M, m), dtype=dtype, device=dev)
-        _, qp, qn = _flat_ptr(q)
-        _, ap, an = _flat_ptr(a1)
+        # the contiguous copies (when q / a1 / a2 are strided views) must outlive the
+        # launch: the caching allocator would hand their blocks to the next torch.empty
+        qc, qp, qn = _flat_ptr(q)
+        a1c, ap, an = _flat_ptr(a1)
         a2f = a2 if a2.dtype == torch.float32 else a2.to(torch.float32)
         a2f, bp, bn = _flat_ptr(a2f)
         if an == 0 or bn == 0:
             raise ZeroDivisionError("integer division or modulo by zero (empty absmax)")
-        keep.append(a2f)
+        keep.extend((qc, a1c, a2f))
         mats[i] = _lib.GemmMat(qp, qn, ap, an, bp, bn, y.data_ptr(), m)
         ys.append(y)
     L = _lib.lib()

@@ -407,3 +407,44 @@ def test_host_activation_is_rejected(gpu):
         nf4_linear(x, mod)
     with pytest.raises(RuntimeError):
         nf4_linear_grouped(x, [mod, mod])
+
+
+@pytest.mark.parametrize("ks", [11, 12, 15])
+def test_k128_slices_starting_past_the_end(coracle, gpu, ks):
+    """K = 4096 (32 chunks of 128) with ksplit 11/12/15: ceil(32/ks) chunks per slice
+    leaves the last slice(s) starting past the end; they must be empty (no wrapped
+    scale-table count, no reads past absmax), single and grouped, table on."""
+    import ctypes
+
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    M, K, Ns = 20, 4096, (256, 128)
+    mats = (_lib.GemmMat * len(Ns))()
+    ys, keep, Ws = [], [], []
+    for i, N in enumerate(Ns):
+        packed, a1, a2 = O.make_inputs(N, K, seed=77 * N + ks, a2_kind="normal")
+        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16))
+        t = [torch.from_numpy(v).to(gpu) for v in (packed, a1, a2)]
+        keep.append(t)
+        y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+        ys.append(y)
+        mats[i] = _lib.GemmMat(t[0].data_ptr(), t[0].numel(), t[1].data_ptr(), t[1].numel(), t[2].data_ptr(),
+                               t[2].numel(), y.data_ptr(), N)
+    xt, xb = _x_bits(M, K, "bf16", seed=ks)
+    x = xt.to(gpu)
+    c = _lib.GemmCfg(_lib.GEMM_K128, 4, 1, ks, 1)
+    wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, mats, len(Ns), ctypes.byref(c))
+    ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=gpu)
+    rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, mats, len(Ns), _lib.BF16, ws.data_ptr(), wsz, ctypes.byref(c),
+                                torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    for y, W in zip(ys, Ws):
+        _check(y, xb, W, "bf16")
+    # single-weight entry point with the same cfg
+    y = torch.full((M, Ns[0]), float("nan"), dtype=torch.bfloat16, device=gpu)
+    rc = _gemm_cfg_call(L, _lib, x, keep[0], y, _lib.BF16, Ns[0], K, c)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    _check(y, xb, Ws[0], "bf16")
