@@ -15,6 +15,7 @@ import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libnf4dq.so")
+EXT_PATH = os.path.join(_HERE, "_lib", "nf4ext.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nf4_dequant.h")
 
 F16 = 0
@@ -130,6 +131,29 @@ def lib() -> ctypes.CDLL:
                 fn.argtypes = args
             _lib = handle
     return _lib
+
+
+_ext = None
+_ext_tried = False
+
+
+def ext():
+    """The tensor-level fast entry (``_lib/nf4ext.so``, csrc/nf4_torch_ext.cpp), or None
+    when it is not built: callers then take the ctypes route to the same kernels."""
+    global _ext, _ext_tried
+    if not _ext_tried:
+        lib()  # the C ABI first (the extension links it; one copy per process); takes _lock itself
+        with _lock:
+            if not _ext_tried:
+                if os.path.exists(EXT_PATH):
+                    import importlib.util
+
+                    spec = importlib.util.spec_from_file_location("nf4ext", EXT_PATH)
+                    mod = importlib.util.module_from_spec(spec)
+                    spec.loader.exec_module(mod)
+                    _ext = mod
+                _ext_tried = True
+    return _ext
 
 
 def strerror(code: int) -> str:

@@ -191,6 +191,7 @@ def _launch_cpu(qweight, absmax, absmax32, out, m, n, code) -> None:
 _REF = None  # bound nf4_dequant_ref (fast path: one attribute lookup less per call)
 _raw_stream = torch._C._cuda_getCurrentRawStream  # device index -> hipStream_t of the current stream
 _U8, _F32 = torch.uint8, torch.float32
+_EXT = _lib.ext()  # tensor-level fast entry (csrc/nf4_torch_ext.cpp), None when not built
 
 
 def _dequantize(qweight, absmax, absmax32, dtype, m, n) -> torch.Tensor:
@@ -199,6 +200,12 @@ def _dequantize(qweight, absmax, absmax32, dtype, m, n) -> torch.Tensor:
         # fp64 output = the fp32 product, widened exactly
         return _dequantize(qweight, absmax, absmax32, torch.float32, m, n).to(torch.float64)
     code = _dtype_code(dtype)  # raise before allocating
+    if _EXT is not None:
+        # uint8 / uint8 / fp32 contiguous device tensors: checks, allocation, stream
+        # and launch in one C++ call (None = this call needs the general path below)
+        out = _EXT.dequant_ref(qweight, absmax, absmax32, m, n, code)
+        if out is not None:
+            return out
     dev = qweight.device
     if dev.type != "cuda":
         if dev.type != "cpu" or backend() != "cpu":

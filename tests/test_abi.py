@@ -114,3 +114,16 @@ def test_cfg_validation():
         cfg = _lib.LaunchCfg(*bad)
         assert L.nf4_dequant_ref_cfg(FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, ctypes.byref(cfg), None) == \
             _lib.ERR_ARG, bad
+
+
+def test_tensor_fast_entry_loads_and_declines_host_tensors():
+    """csrc/nf4_torch_ext.cpp is built in-tree and loads beside libnf4dq.so; host
+    tensors (and anything else off its fast path) come back as None, never computed."""
+    import torch
+
+    from nf4_triton_dequantization_amd import kernel
+
+    E = _lib.ext()
+    assert E is not None and kernel._EXT is E
+    q = torch.zeros(64, dtype=torch.uint8)
+    assert E.dequant_ref(q, torch.ones(2, dtype=torch.uint8), torch.ones(1), 2, 64, _lib.BF16) is None

@@ -8,7 +8,8 @@ result), ``iterations`` times between two events; the total seconds is the
 number the reference compares against unsloth.  unsloth/peft/bitsandbytes are
 absent here, so only this path's time is reported, together with the device
 time the same dequantizations need (hipGraph replay) -- the gap between the two
-is host launch overhead (Python + ctypes + allocation per call).
+is host launch overhead (Python + ctypes + allocation per call).  Unlike the
+reference loop, the end event waits for all three streams.
 
 Also reports the per-call host cost of ``triton_dequantize_nf4`` alone.
 """
@@ -50,6 +51,13 @@ def mlp_dequantize(mlp, fx, sync=True):
         c = fx(mlp.down_proj).t()
     if sync:
         torch.cuda.synchronize()
+    else:
+        # the timing event is recorded on the current stream: make it wait for the
+        # three side streams, or it can fire before their work is done (the
+        # reference's benchmark.py:116-126 has that flaw; not copied)
+        cur = torch.cuda.current_stream()
+        for s in (s1, s2, s3):
+            cur.wait_stream(s)
     return a, b, c
 
 
@@ -104,7 +112,31 @@ def main():
         triton_dequantize_nf4(lin)
     host_us = (time.perf_counter() - t0) * 1e6 / n
     torch.cuda.synchronize()
-    print(json.dumps({"reference_style_total_seconds": total, "api_host_us_per_call": host_us}), flush=True)
+    # the same call on a duck-typed module holding plain tensors (no nn.Parameter
+    # `.data` re-wrap per call) -- what is left is this path's own cost
+    from types import SimpleNamespace
+
+    w = lin.weight
+    duck = SimpleNamespace(weight=SimpleNamespace(data=w.data, quant_state=w.quant_state),
+                           out_features=lin.out_features, in_features=lin.in_features)
+    for _ in range(20):
+        triton_dequantize_nf4(duck)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        triton_dequantize_nf4(duck)
+    duck_us = (time.perf_counter() - t0) * 1e6 / n
+    torch.cuda.synchronize()
+    # torch's own floor for comparison: one allocation of the output per call
+    torch.cuda._sleep(200_000_000)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        torch.empty((4096, 4096), dtype=torch.bfloat16, device="cuda")
+    empty_us = (time.perf_counter() - t0) * 1e6 / n
+    torch.cuda.synchronize()
+    print(json.dumps({"reference_style_total_seconds": total, "api_host_us_per_call": host_us,
+                      "api_host_us_per_call_plain_tensors": duck_us, "torch_empty_us": empty_us}), flush=True)
 
 
 if __name__ == "__main__":
