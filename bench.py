@@ -1,34 +1,52 @@
-"""Benchmark: NF4 -> bf16 double dequantization of a 4096x4096 weight on MI355X.
+"""Benchmark: NF4 double dequantization on MI355X (BASELINE.json metric).
 
 Metric (BASELINE.json): dequantized elements/s + achieved HBM GB/s, 4096x4096
-NF4->bf16 (configs[1]).  A *step* is one dequantization of one 4096x4096
-weight through the product C ABI (``nf4_dequant_ref``), inputs resident in HBM.
+NF4->bf16 (configs[1]).  A *step* is one pass of the hot path over one batch:
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+* ``--workload c2`` (default; the headline): one 4096x4096 NF4->bf16 weight per
+  rank through the C ABI (``nf4_dequant_ref``); weak scaling (each rank its own
+  matrix);
+* ``--workload c5`` (BASELINE configs[4]): the 8 independent 8192x8192 matrices,
+  split round-robin over the ranks (one per GPU at N=8), each rank's share in one
+  batched launch (``nf4_dequant_ref_batched``); strong scaling (the 8-matrix job
+  is fixed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Timed region (the ``value``): K steps captured once into a hipGraph and
-replayed, bracketed by barrier + synchronize on both sides; step i reads and
-writes buffer set i % P, with P sets (P * 42 MB >> the 256 MiB Infinity Cache)
-so every step streams from and to HBM.  ``value`` = elements of all ranks / max
-over ranks of the region time.
+``--gpus N`` without a launcher (WORLD_SIZE unset) spawns N fresh rank processes
+before this process touches the GPU and relays rank 0's line; under a launcher
+WORLD_SIZE must equal N.
+
+Timed region (``value``): K steps captured once into a hipGraph and replayed,
+bracketed by barrier + synchronize on both sides.  Step i uses buffer set
+i % P; P is chosen so each rank's sets span >= 1 GiB (>> the 256 MiB Infinity
+Cache), and a 512 MiB scratch write between the untimed replay and the timed one
+evicts whatever the untimed pass left cached.  ``value`` = elements of all ranks
+/ max over ranks of the region time.
 
 Roofline (``roofline``): ``achieved`` = algorithmic bytes per launch (SURVEY
 §8d: N/2 packed + 2N out + nb absmax + 4*min(n2, m*G) nested absmax) / mean
-launch duration, the latter from the HIP events that bracket the timed region
-on the launch stream (region time / K: inter-launch gaps count against us);
-``peak`` = 8 TB/s; ``traffic`` = PMC-counted HBM bytes per launch from
-profiles/<round>/pmc_traffic.json (tools/pmc_traffic.py) when present.
+launch duration = HIP-event time of the timed region on the launch stream / K
+(inter-launch gaps count against us); ``peak`` = 8 TB/s; ``traffic`` =
+PMC-counted HBM bytes per launch from profiles/<round>/pmc_traffic.json
+(tools/pmc_traffic.py) when present for this shape.
 
-CPU baseline (``cpu_baseline``, rank 0 at N=1), same 4096x4096 workload on this
-GPU's host share of cores (at most 16): ``value`` = oracle/fallback_torch.py, a
+CPU baseline (``cpu_baseline``, rank 0 at N=1), same workload on this GPU's
+host share of cores (at most 16): ``value`` = oracle/fallback_torch.py, a
 torch-CPU restatement with the reference fallback's loop structure (the CPU path
-the reference itself runs); ``native`` = the C oracle over OpenMP threads;
-``single_thread`` = the C oracle on one thread.
+the reference itself runs, bit-equal to it); ``native`` = this library's own
+host path ``nf4_dequant_ref_cpu`` (AVX2, same threads); ``single_thread`` = the
+same at 1 thread.
 
-Multi-GPU (weak scaling): every rank dequantizes its own matrices; rank 0 owns
-the quant statistics of all ranks' matrices and broadcasts them once over RCCL
-at setup (sharding.broadcast_quant_stats) -- no collective on the data path.
+``--backend cpu`` runs the steps through ``nf4_dequant_ref_cpu`` on host memory
+(wall-clock timing, no roofline): the rehearsal mode the CPU tests use to drive
+the spawn / gloo / max-over-ranks path without a GPU.
+
+Multi-GPU: every rank dequantizes its own matrices; rank 0 owns the quant
+statistics of every rank's matrices and broadcasts them once over RCCL at setup
+(sharding.broadcast_quant_stats, timed and reported separately) -- no
+collective on the data path.
 """
 from __future__ import annotations
 
@@ -36,69 +54,109 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from nf4_triton_dequantization_amd import _lib  # noqa: E402
-from nf4_triton_dequantization_amd.sharding import QuantStats, broadcast_quant_stats, max_over_ranks  # noqa: E402
-
 PEAK_HBM = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
-ROUND = "r01"
-
-
-def algorithmic_bytes(m: int, n: int, out_bytes: int, nb: int, n2: int) -> int:
-    """packed + output + u8 absmax + unique fp32 nested absmax."""
-    N = m * n
-    bpr = (n + 63) // 64
-    groups = (bpr + 3) // 4
-    return N // 2 + N * out_bytes + nb + 4 * min(n2, m * groups)
+ROUNDS = ("r02", "r01")  # profiles/<round>/pmc_traffic.json, newest first
+MIN_FOOTPRINT = 1 << 30  # bytes of buffer sets per rank (>> 256 MiB Infinity Cache)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def gen_set(m, n, seed, rank):
-    """Packed weight for (rank, set) from the shared splitmix64 generator."""
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c5"])
+    ap.add_argument("--m", type=int, default=None, help="override the c2 matrix shape (rows)")
+    ap.add_argument("--n", type=int, default=None, help="override the c2 matrix shape (columns)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
+    ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = enough for >= 1 GiB)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-flush", action="store_true", help="skip the Infinity-Cache flush before timing")
+    ap.add_argument("--tile-dwords", type=int, default=4)
+    ap.add_argument("--blocks-per-cu", type=int, default=0)
+    ap.add_argument("--nontemporal", type=int, default=1)
+    ap.add_argument("--flags", type=int, default=0, help="NF4DQ_CFG_* bits (1 = nt loads)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])
+    ap.add_argument("--dist-backend", default=None, help="nccl (= RCCL, default on GPUs) or gloo (rehearsal)")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launcher: N fresh rank processes (no GPU call in this process)
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """Run this script as N ranks (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), relay their
+    output, return the worst exit code.  The parent never initialises the GPU, so
+    the children are plain fresh processes (no exec from a GPU-initialised one)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# ---------------------------------------------------------------------------
+# workload
+# ---------------------------------------------------------------------------
+def rank_matrices(args, rank: int, world: int):
+    """[(global matrix id, m, n)] this rank dequantizes per step."""
+    if args.workload == "c5":
+        import workloads as W
+
+        m, n = W.C5_SHAPE
+        return [(i, m, n) for i in range(rank, W.C5_MATRICES, world)]
+    m = args.m or 4096
+    n = args.n or 4096
+    return [(rank, m, n)]
+
+
+def algorithmic_bytes(m, n, out_bytes, nb, n2):
+    import workloads as W
+
+    return W.algorithmic_bytes(m, n, out_bytes, nb, n2)
+
+
+def cpu_baseline(shapes, seconds, dtype_code):
+    """CPU figures on the same workload (the rank's step), on this GPU's host share
+    of cores (<= 16): the reference fallback's structure in torch-CPU (``value``),
+    this library's host path (``native``) and the same at one thread."""
+    import torch
+
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import nf4_oracle as O  # input generator (deterministic); not on the measured path
+    import fallback_torch as F  # the baseline's reference-structure port (checker side)
+    import workloads as W
+    from nf4_triton_dequantization_amd import _lib
 
-    return O.splitmix64_bytes(seed * 1000003 + rank, m * n // 2, stream=1)
-
-
-def gen_stats(m, n, seed):
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import nf4_oracle as O
-
-    nb = (m * n + 63) // 64
-    n2 = (nb + 255) // 256
-    return O.splitmix64_bytes(seed, nb, stream=2), O.uniform_f32(seed, n2, 1e-3, 1e-2, stream=3)
-
-
-def cpu_baseline(m, n, seconds, dtype_code):
-    """CPU figures on the same workload, on this GPU's host share of cores (<= 16):
-
-    * ``value``: oracle/fallback_torch.py -- torch-CPU restatement with the
-      reference fallback's execution shape (kernel_optimized.py:208-314: per-block
-      scale loop, per-column strided writes), the "reference fallback" row of
-      BASELINE.md's CPU plan; ~`seconds` of repeats;
-    * ``native``: the C oracle, rows over OpenMP threads (~`seconds`/2);
-    * ``single_thread``: the C oracle on one thread (~`seconds`/4).
-    """
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import fallback_torch as F
-    import nf4_oracle as O
-
-    c = O.COracle()
-    p, a1, a2 = O.make_inputs(m, n, 3409)
+    L = _lib.lib()
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
+    m, n = shapes[0][1], shapes[0][2]
+    p, a1, a2 = W.make_inputs(m, n, 3409)
+    elems = m * n
 
     def repeat(fn, secs):
         fn()  # warm (page-in, thread pool)
@@ -111,7 +169,7 @@ def cpu_baseline(m, n, seconds, dtype_code):
             if el >= secs:
                 return reps, el
 
-    tdt = torch.bfloat16 if dtype_code == O.BF16 else torch.float16
+    tdt = torch.bfloat16 if dtype_code == _lib.BF16 else torch.float16
     tp, ta1, ta2 = torch.from_numpy(p), torch.from_numpy(a1), torch.from_numpy(a2)
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
@@ -119,195 +177,257 @@ def cpu_baseline(m, n, seconds, dtype_code):
         rf, ef = repeat(lambda: F.dequant_fallback(tp, ta1, ta2, m, n, tdt), seconds)
     finally:
         torch.set_num_threads(prev)
+    out = np.empty((m, n), np.uint16)
 
     def native(nthreads, secs):
-        c.set_threads(nthreads)
-        return repeat(lambda: c.dequant_ref(p, a1, a2, m, n, dtype_code), secs)
+        def once():
+            rc = L.nf4_dequant_ref_cpu(p.ctypes.data, p.size, a1.ctypes.data, a1.size, a2.ctypes.data, a2.size,
+                                       out.ctypes.data, dtype_code, m, n, nthreads)
+            if rc:
+                raise RuntimeError(f"nf4_dequant_ref_cpu: {_lib.strerror(rc)}")
+        return repeat(once, secs)
 
-    rn, en = native(threads, max(1.0, seconds / 2))
+    rn, en = native(threads, max(1.0, seconds / 4))
     r1, e1 = native(1, max(1.0, seconds / 4))
-    c.set_threads(1)
-    dname = "bf16" if dtype_code == O.BF16 else "fp16"
-    return {"value": rf * m * n / ef, "unit": "elements/s", "cores": threads, "kind": "port",
+    dname = "bf16" if dtype_code == _lib.BF16 else "fp16"
+    return {"value": rf * elems / ef, "unit": "elements/s", "cores": threads, "kind": "port",
             "sample": f"{rf} x {m}x{n} NF4->{dname} by oracle/fallback_torch.py (the reference fallback's "
-                      f"loop structure in torch-CPU, {threads} threads), {ef:.1f} s",
-            "native": {"value": rn * m * n / en, "cores": threads,
-                       "sample": f"{rn} x {m}x{n} by oracle/nf4_oracle.c (scalar C, rows over {threads} "
-                                 f"OpenMP threads), {en:.1f} s"},
-            "single_thread": {"value": r1 * m * n / e1, "cores": 1,
-                              "sample": f"{r1} x {m}x{n} by oracle/nf4_oracle.c, 1 thread, {e1:.1f} s"}}
+                      f"loop structure in torch-CPU, bit-equal to it, {threads} threads), {ef:.1f} s",
+            "native": {"value": rn * elems / en, "cores": threads,
+                       "sample": f"{rn} x {m}x{n} by libnf4dq.so nf4_dequant_ref_cpu (this library's host path, "
+                                 f"AVX2 table lookups, {threads} threads), {en:.1f} s"},
+            "single_thread": {"value": r1 * elems / e1, "cores": 1,
+                              "sample": f"{r1} x {m}x{n} by nf4_dequant_ref_cpu, 1 thread, {e1:.1f} s"}}
+
+
+def find_traffic(m, n, dtype):
+    for rnd in ROUNDS:
+        path = os.path.join(REPO, "profiles", rnd, "pmc_traffic.json")
+        if not os.path.exists(path):
+            continue
+        try:
+            with open(path) as f:
+                pmc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if pmc.get("m") == m and pmc.get("n") == n and pmc.get("dtype") == dtype:
+            return pmc.get("hbm_bytes_per_launch"), f"profiles/{rnd}/pmc_traffic.json"
+    return None, None
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--m", type=int, default=4096)
-    ap.add_argument("--n", type=int, default=4096)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
-    ap.add_argument("--sets", type=int, default=16, help="rotating buffer sets (>256 MiB total)")
-    ap.add_argument("--streams", type=int, default=1, help="streams the steps round-robin over")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--tile-dwords", type=int, default=4)
-    ap.add_argument("--blocks-per-cu", type=int, default=0)
-    ap.add_argument("--nontemporal", type=int, default=1)
-    ap.add_argument("--flags", type=int, default=0, help="NF4DQ_CFG_* bits (1 = nt loads)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for real runs; gloo to rehearse")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    args = parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; they must agree")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal on a box with fewer GPUs than ranks (gloo only): ranks share devices
-    ndev = torch.cuda.device_count()
-    local_dev = local if args.dist_backend == "nccl" else local % max(1, ndev)
-    torch.cuda.set_device(local_dev)
-    dev = torch.device("cuda", local_dev)
+
+    import torch
+    import torch.distributed as dist
+
+    from nf4_triton_dequantization_amd import _lib
+    from nf4_triton_dequantization_amd.sharding import QuantStats, broadcast_quant_stats, max_over_ranks
+    import workloads as W
+
+    cpu = args.backend == "cpu"
+    dist_backend = args.dist_backend or ("gloo" if cpu else "nccl")
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        # rehearsal with more ranks than GPUs (gloo only): ranks share devices
+        ndev = torch.cuda.device_count()
+        local_dev = local if dist_backend == "nccl" else local % max(1, ndev)
+        torch.cuda.set_device(local_dev)
+        dev = torch.device("cuda", local_dev)
     if world > 1:
-        if args.dist_backend == "nccl":
+        if dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(dist_backend)
 
-    m, n, P = args.m, args.n, args.sets
+    mats = rank_matrices(args, rank, world)
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
     code = _lib.BF16 if args.dtype == "bf16" else _lib.F16
     L = _lib.lib()
 
-    # ---- setup: resident inputs, quant stats broadcast from rank 0 ----------
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
+    # ---- setup: quant stats of every rank's matrices on rank 0, broadcast once ----
+    step_bytes = sum(m * n // 2 + 2 * m * n for _, m, n in mats)  # packed + output per step (this rank)
+    P = args.sets or max(2, -(-MIN_FOOTPRINT // max(1, step_bytes)))
+    if cpu:
+        P = args.sets or 2
+    all_mats = [rank_matrices(args, r, world) for r in range(world)]
     t_setup = time.perf_counter()
     if rank == 0:
         stats = []
         for r in range(world):
             for s in range(P):
-                a1, a2 = gen_stats(m, n, 3409 + 7919 * r + s)
-                stats.append(QuantStats(m, n, torch.from_numpy(a1), torch.from_numpy(a2), dt))
+                for gid, m, n in all_mats[r]:
+                    seed = 3409 + 7919 * gid + 104729 * s
+                    nb = m * n // 64
+                    stats.append(QuantStats(m, n, torch.from_numpy(W.splitmix64_bytes(seed, nb, stream=2)),
+                                            torch.from_numpy(W.uniform_f32(seed, (nb + 255) // 256, 1e-3, 1e-2,
+                                                                           stream=3)), dt))
     else:
         stats = None
     if world > 1:
-        torch.cuda.synchronize()
+        sync()
         tb = time.perf_counter()
         stats = broadcast_quant_stats(stats, dev, src=0)
-        torch.cuda.synchronize()
+        sync()
         bcast_ms = (time.perf_counter() - tb) * 1e3
     else:
         stats = [QuantStats(s.m, s.n, s.absmax.to(dev), s.absmax2.to(dev), s.dtype) for s in stats]
         bcast_ms = 0.0
-    mine = stats[rank * P:(rank + 1) * P]
-    sets = []
+    per_rank = P * len(mats)
+    mine = stats[rank * per_rank:(rank + 1) * per_rank]
+    sets = []  # sets[s] = [(q, a1, a2, out, m, n)] for this rank's matrices
+    k = 0
     for s in range(P):
-        q = torch.from_numpy(gen_set(m, n, 3409 + s, rank)).to(dev)
-        out = torch.empty((m, n), dtype=dt, device=dev)
-        sets.append((q, mine[s].absmax, mine[s].absmax2, out))
-    torch.cuda.synchronize()
-    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s, quant_state broadcast {bcast_ms:.2f} ms")
+        row = []
+        for gid, m, n in mats:
+            seed = 3409 + 7919 * gid + 104729 * s
+            q = torch.from_numpy(W.splitmix64_bytes(seed, m * n // 2, stream=1)).to(dev)
+            out = torch.empty((m, n), dtype=dt, device=dev)
+            row.append((q, mine[k].absmax, mine[k].absmax2, out, m, n))
+            k += 1
+        sets.append(row)
+    sync()
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s, {P} buffer sets x {len(mats)} matrices, "
+        f"quant_state broadcast {bcast_ms:.2f} ms")
 
     cfg = _lib.LaunchCfg(args.tile_dwords, args.blocks_per_cu, args.nontemporal, args.flags)
     cfg_p = ctypes.byref(cfg)
+    descs = []
+    for row in sets:
+        arr = (_lib.MatrixDesc * len(row))(*[
+            _lib.MatrixDesc(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                            out.data_ptr(), m, n) for (q, a1, a2, out, m, n) in row])
+        descs.append(arr)
 
-    def launch(i, stream_ptr):
-        q, a1, a2, out = sets[i % P]
-        rc = L.nf4_dequant_ref_cfg(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
-                                   out.data_ptr(), code, m, n, cfg_p, stream_ptr)
-        if rc:
-            raise RuntimeError(f"nf4_dequant_ref_cfg: {_lib.strerror(rc)}")
-
-    main_stream = torch.cuda.current_stream(dev)
-    side = [torch.cuda.Stream(dev) for _ in range(max(0, args.streams - 1))]
-
-    def issue(k0, count):
-        """Steps k0..k0+count-1 round-robin over main + side streams."""
-        if not side:
-            ptr = torch.cuda.current_stream(dev).cuda_stream
-            for i in range(k0, k0 + count):
-                launch(i, ptr)
+    def launch(i):
+        row = sets[i % P]
+        if cpu:
+            for (q, a1, a2, out, m, n) in row:
+                rc = L.nf4_dequant_ref_cpu(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(),
+                                           a2.numel(), out.data_ptr(), code, m, n, 0)
+                if rc:
+                    raise RuntimeError(f"nf4_dequant_ref_cpu: {_lib.strerror(rc)}")
             return
-        cur = torch.cuda.current_stream(dev)
-        streams = [cur] + side
-        for s in side:
-            s.wait_stream(cur)
-        for i in range(k0, k0 + count):
-            launch(i, streams[i % len(streams)].cuda_stream)
-        for s in side:
-            cur.wait_stream(s)
+        sp = torch.cuda.current_stream(dev).cuda_stream
+        if len(row) == 1:
+            q, a1, a2, out, m, n = row[0]
+            rc = L.nf4_dequant_ref_cfg(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(),
+                                       a2.numel(), out.data_ptr(), code, m, n, cfg_p, sp)
+        else:
+            rc = L.nf4_dequant_ref_batched(descs[i % P], len(row), code, sp)
+        if rc:
+            raise RuntimeError(f"nf4 dequant launch: {_lib.strerror(rc)}")
 
-    # correctness sanity of set 0 against the oracle (the tests do the full job)
-    issue(0, 1)
-    torch.cuda.synchronize()
+    # correctness sanity of set 0 against the oracle on the first 64 rows of each
+    # matrix (the checker; tests/ do the full job)
+    launch(0)
+    sync()
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import nf4_oracle as O
 
-    q0, a10, a20, o0 = sets[0]
-    rows = slice(0, 64)
-    want = O.dequant_ref_np(q0[: 64 * n // 2].cpu().numpy(), a10.cpu().numpy(), a20.cpu().numpy(), 64, n,
-                            O.BF16 if args.dtype == "bf16" else O.F16)
-    got = o0[rows].contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
-    if not np.array_equal(got, want):
-        raise RuntimeError("bench sanity check failed: HIP output differs from the oracle")
+    for (q, a1, a2, out, m, n) in sets[0]:
+        want = O.dequant_ref_np(q[: 64 * n // 2].cpu().numpy(), a1.cpu().numpy(), a2.cpu().numpy(), 64, n,
+                                O.BF16 if args.dtype == "bf16" else O.F16)
+        got = out[:64].contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+        if not np.array_equal(got, want):
+            raise RuntimeError("bench sanity check failed: output differs from the oracle")
 
-    # ---- warmup + graph capture ----------------------------------------------
+    # ---- warmup + graph capture ------------------------------------------------------
     for w in range(args.warmup):
-        issue(w, 1)
-    torch.cuda.synchronize()
+        launch(w)
+    sync()
     graph = None
-    if not args.no_graph:
+    if not cpu and not args.no_graph:
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                issue(0, args.steps)
+                for i in range(args.steps):
+                    launch(i)
             graph.replay()  # upload + one untimed pass
             torch.cuda.synchronize()
         except Exception as e:  # capture unsupported -> eager issue, reported in config
             log(f"[rank {rank}] hipGraph capture failed ({e}); timing eager launches")
             graph = None
             torch.cuda.synchronize()
+    if not cpu and not args.no_flush:
+        # evict what the untimed pass left in the Infinity Cache (its last sets are
+        # the timed pass's first ones when K is not a multiple of P)
+        scratch = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+        scratch.fill_(1)
+        torch.cuda.synchronize()
+        del scratch
 
-    # ---- timed region -----------------------------------------------------------
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    # ---- timed region --------------------------------------------------------------------
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    ev0.record(main_stream)
-    if graph is not None:
-        graph.replay()
+    sync()
+    if cpu:
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            launch(i)
+        t_ms = (time.perf_counter() - t0) * 1e3
     else:
-        issue(0, args.steps)
-    ev1.record(main_stream)
-    torch.cuda.synchronize()
+        main_stream = torch.cuda.current_stream(dev)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(main_stream)
+        if graph is not None:
+            graph.replay()
+        else:
+            for i in range(args.steps):
+                launch(i)
+        ev1.record(main_stream)
+        torch.cuda.synchronize()
+        t_ms = ev0.elapsed_time(ev1)
     if world > 1:
         dist.barrier()
-    t_ms = ev0.elapsed_time(ev1)
+    my_ms = t_ms
+    per_rank_ms = [my_ms]
     if world > 1:
-        t_ms = max_over_ranks(t_ms, dev)
+        t_ms = max_over_ranks(my_ms, dev)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, my_ms)
+        per_rank_ms = gathered
 
-    # ---- roofline: mean launch duration = HIP-event time of the timed region / K
-    # (events on the launch stream; includes the inter-launch gaps, so it is an
-    # upper bound on the rocprof per-kernel duration committed under profiles/).
-    kt_mean = t_ms * 1e3 / args.steps  # us
-
-    out_b = 2
-    nb, n2 = sets[0][1].numel(), sets[0][2].numel()
-    alg = algorithmic_bytes(m, n, out_b, nb, n2)
-    achieved = alg / (kt_mean * 1e-6)
-    traffic = None
-    pmc_path = os.path.join(REPO, "profiles", ROUND, "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            if pmc.get("m") == m and pmc.get("n") == n and pmc.get("dtype") == args.dtype:
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
-
-    elems = m * n * args.steps * world
-    value = elems / (t_ms * 1e-3)
+    # ---- figures -------------------------------------------------------------------------------
+    my_elems = sum(m * n for _, m, n in mats)
+    my_alg = sum(algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256) for _, m, n in mats)
+    launches_per_step = 1 if not cpu else len(mats)
+    all_elems = sum(m * n for r in range(world) for _, m, n in all_mats[r])
+    all_alg = sum(algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256)
+                  for r in range(world) for _, m, n in all_mats[r])
+    value = all_elems * args.steps / (t_ms * 1e-3)
+    kt_mean = my_ms * 1e3 / (args.steps * launches_per_step)  # us per launch, this rank
+    m0, n0 = mats[0][1], mats[0][2]
+    traffic, traffic_src = (None, None)
+    if not cpu and len(mats) == 1:
+        traffic, traffic_src = find_traffic(m0, n0, args.dtype)
+    achieved = my_alg / launches_per_step / (kt_mean * 1e-6)
+    if args.workload == "c5":
+        metric = "dequantized elements/s (8 x 8192x8192 NF4->bf16, one matrix per GPU at N=8)"
+        workload = (f"c5: 8 independent 8192x8192 NF4->{args.dtype} matrices (BASELINE configs[4]) split "
+                    f"round-robin over {world} rank(s), each rank's share in one batched launch per step")
+        scaling = "strong"
+    else:
+        metric = "dequantized elements/s (4096x4096 NF4->bf16, blocksize 64 / nested 256)"
+        workload = (f"c2: {m0}x{n0} NF4->{args.dtype} double dequant (BASELINE configs[1]), one matrix per rank "
+                    f"per step")
+        scaling = "weak"
     res = {
-        "metric": "dequantized elements/s (4096x4096 NF4->bf16, blocksize 64 / nested 256)",
+        "metric": metric,
         "value": value,
         "unit": "elements/s",
         "n_gpus": world,
@@ -315,35 +435,43 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": t_ms / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (splitmix64 packed weights + absmax, resident in HBM)",
-        "hbm_gb_s": value * alg / (m * n) / 1e9,
+        "hbm_gb_s": all_alg * args.steps / (t_ms * 1e-3) / 1e9,
+        "per_rank": [{"rank": r, "ms_per_step": per_rank_ms[r] / args.steps,
+                      "elements_per_s": sum(m * n for _, m, n in all_mats[r]) * args.steps / (per_rank_ms[r] * 1e-3),
+                      "GBps": sum(algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256)
+                                  for _, m, n in all_mats[r]) * args.steps / (per_rank_ms[r] * 1e-3) / 1e9}
+                     for r in range(world)],
         "config": {
-            "workload": f"{m}x{n} NF4->{args.dtype} double dequant (BASELINE configs[1]), one matrix per step",
-            "m": m, "n": n, "out_dtype": args.dtype, "arith": "u8 unpack, fp32 scale/multiply, RNE to bf16",
-            "buffer_sets": P, "launch": "hipGraph" if graph is not None else "eager",
-            "streams": args.streams, "tile_dwords": args.tile_dwords, "blocks_per_cu": args.blocks_per_cu,
-            "nontemporal": args.nontemporal, "flags": args.flags, "parallelism": f"shard{world} (independent matrices)",
-            "quant_state_broadcast_ms": round(bcast_ms, 3), "dist_backend": args.dist_backend if world > 1 else None,
+            "workload": workload,
+            "matrices_per_rank": len(mats), "m": m0, "n": n0, "out_dtype": args.dtype,
+            "arith": "u8 unpack, fp32 scale/multiply, RNE to bf16/fp16", "backend": args.backend,
+            "buffer_sets": P, "launch": "hipGraph" if graph is not None else ("host loop" if cpu else "eager"),
+            "tile_dwords": args.tile_dwords, "blocks_per_cu": args.blocks_per_cu, "nontemporal": args.nontemporal,
+            "flags": args.flags, "parallelism": f"shard{world} (independent matrices)",
+            "cache_flush_before_timing": not cpu and not args.no_flush,
+            "quant_state_broadcast_ms": round(bcast_ms, 3), "dist_backend": dist_backend if world > 1 else None,
         },
-        "roofline": {
+        "roofline": None if cpu else {
             "bound": "hbm",
             "achieved": achieved / 1e9,
             "peak": PEAK_HBM / 1e9,
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": "nf4_flat_kernel",
             "launch_us_mean": kt_mean,
-            "launch_us_source": "HIP events over the timed region / steps (gaps included)",
-            "algorithmic_bytes_per_launch": alg,
+            "launch_us_source": "HIP events over the timed region on the launch stream / launches (gaps included)",
+            "algorithmic_bytes_per_launch": my_alg // launches_per_step,
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(m, n, args.cpu_seconds, O.BF16 if args.dtype == "bf16" else O.F16)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cpu:
+        res["cpu_baseline"] = cpu_baseline(mats, args.cpu_seconds, code)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -61,13 +61,38 @@ struct Desc {
     uint32_t blk_base;       // scale blocks before this piece (a matrix above kPieceBytes is several pieces)
 };
 
+// Diagnostic build only (tools/Makefile `stamps`): per-wave s_memrealtime stamps of
+// the flat kernel -- entry, first tile decoded and stored (its loads arrived), exit
+// after its stores completed, tiles walked -- into a buffer set by nf4_dbg_set_stamps.
+#ifndef NF4_FLAT_STAMPS
+#define NF4_FLAT_STAMPS 0
+#endif
+
 template <int MAXB>
 struct Batch {
     Desc d[MAXB];
     uint32_t count;
     uint32_t total_tiles;
     uint32_t seg_shift;  // tiles are split into 2^seg_shift contiguous segments, one per block residue
+#if NF4_FLAT_STAMPS
+    unsigned long long* stamps;
+#endif
 };
+
+#if NF4_FLAT_STAMPS
+#define NF4_FSTAMP(slot_, val_)                                                                      \
+    do {                                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                                           \
+        if (lane == 0) bt.stamps[(blockIdx.x * WPG + (threadIdx.x >> 6)) * 4u + (slot_)] = (val_);   \
+        __builtin_amdgcn_sched_barrier(0);                                                           \
+    } while (0)
+#define NF4_FNOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define NF4_FSTAMP(slot_, val_) \
+    do {                        \
+    } while (0)
+#define NF4_FNOW() 0ull
+#endif
 
 // Scalar store of one output element (rows kernels).
 template <int DT>
@@ -269,6 +294,10 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[X4 ? WPG * 256 : 1];
     uint32_t* stage = stage_all + (X4 ? (threadIdx.x >> 6) * 256 : 0);
     const uint32_t lane = threadIdx.x & 63u;
+#if NF4_FLAT_STAMPS
+    const unsigned long long t_entry = NF4_FNOW();
+    unsigned long long tiles_done = 0;
+#endif
     const uint32_t sshift = bt.seg_shift;
     SegMap sm;
     sm.seg_tiles = (bt.total_tiles + (1u << sshift) - 1u) >> sshift;
@@ -294,13 +323,23 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
     }
     write_lut(lut);
     __syncthreads();
-    if (!ca.valid) return;
+    if (!ca.valid) {
+        NF4_FSTAMP(0, t_entry);
+        NF4_FSTAMP(1, 0ull);
+        NF4_FSTAMP(2, NF4_FNOW());
+        NF4_FSTAMP(3, 0ull);
+        return;
+    }
     while (true) {
         const Cursor cb = cursor_at<DT, U>(bt, sm, ca.i + nwaves, ca.k);
         __amdgpu_buffer_rsrc_t rpb = rpa, rob = roa;
         if (MAXB > 1 && cb.k != ca.k) make_rsrcs<DT>(bt, cb.k, rpb, rob);
         const TileIn<U> B = tile_load<DT, MODE, U, AUXL, X4>(bt.d[cb.k], rpb, cb.base, lane);
         tile_finish<DT, MODE, U, AUXS, X4>(bt.d[ca.k], roa, lut, A, ca.base, lane, stage);
+#if NF4_FLAT_STAMPS
+        if (tiles_done == 0) NF4_FSTAMP(1, NF4_FNOW());
+        ++tiles_done;
+#endif
         if (!cb.valid) break;
 
         const Cursor cn = cursor_at<DT, U>(bt, sm, cb.i + nwaves, cb.k);
@@ -308,11 +347,20 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
         if (MAXB > 1 && cn.k != cb.k) make_rsrcs<DT>(bt, cn.k, rpn, ron);
         A = tile_load<DT, MODE, U, AUXL, X4>(bt.d[cn.k], rpn, cn.base, lane);
         tile_finish<DT, MODE, U, AUXS, X4>(bt.d[cb.k], rob, lut, B, cb.base, lane, stage);
+#if NF4_FLAT_STAMPS
+        ++tiles_done;
+#endif
         if (!cn.valid) break;
         ca = cn;
         rpa = rpn;
         roa = ron;
     }
+#if NF4_FLAT_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);  // every load and store of this wave complete
+    NF4_FSTAMP(0, t_entry);
+    NF4_FSTAMP(2, NF4_FNOW());
+    NF4_FSTAMP(3, tiles_done);
+#endif
 }
 
 // Any shape, reference / single-quant semantics: one thread per packed byte.
@@ -395,6 +443,10 @@ inline int ilog2(uint64_t v) {
 
 constexpr nf4_launch_cfg kDefaultCfg = {4, 0, 1, 0};  // measured best at 4096^2 (tools/tune.py)
 
+#if NF4_FLAT_STAMPS
+unsigned long long* g_stamps = nullptr;  // diagnostic build: [wave][4] u64
+#endif
+
 int cu_count() {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 256;
@@ -472,6 +524,9 @@ int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_laun
     const uint64_t S = uint64_t(1) << sshift;
     blocks = (blocks + S - 1) / S * S;  // every segment gets the same number of blocks
 
+#if NF4_FLAT_STAMPS
+    b.stamps = g_stamps;
+#endif
     const uint32_t pol = (uint32_t)((cfg.flags >> NF4DQ_CFG_STORE_POLICY_BIT) & 0xF);
     if (cfg.flags & NF4DQ_CFG_X4_LOADS) {  // 16 B/lane loads + LDS redistribution: base shape only
         if (U != 4 || wpg != 4 || !cfg.nontemporal || pol) return NF4DQ_ERR_ARG;
@@ -848,6 +903,11 @@ const char* nf4_strerror(int code) {
     return "unknown error";
 }
 
-const char* nf4_version(void) { return "nf4dq 0.1.0 gfx950"; }
+const char* nf4_version(void) { return "nf4dq 0.2.0 gfx950"; }
+
+#if NF4_FLAT_STAMPS
+// Diagnostic build only: where the flat kernel writes its per-wave stamps.
+void nf4_dbg_set_stamps(void* buf) { g_stamps = reinterpret_cast<unsigned long long*>(buf); }
+#endif
 
 }  // extern "C"
