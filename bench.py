@@ -19,11 +19,15 @@ before this process touches the GPU and relays rank 0's line; under a launcher
 WORLD_SIZE must equal N.
 
 Timed region (``value``): K steps captured once into a hipGraph and replayed,
-bracketed by barrier + synchronize on both sides.  Step i uses buffer set
-i % P; P is chosen so each rank's sets span >= 1 GiB (>> the 256 MiB Infinity
-Cache), and a 512 MiB scratch write between the untimed replay and the timed one
-evicts whatever the untimed pass left cached.  ``value`` = elements of all ranks
-/ max over ranks of the region time.
+bracketed by barrier + synchronize on both sides, HIP events on the launch
+stream around the replay; one more untimed replay is enqueued right ahead of the
+start event (no host sync in between), so the timed steps follow warm steps back
+to back and the host's submission latency is hidden behind it.  Step i uses buffer set i % P; P is chosen so
+each rank's sets span >= 1 GiB (>> the 256 MiB Infinity Cache) and so that a set
+is reused >= 256 MiB of traffic later across the untimed -> timed replay
+boundary (profiles/r02/bench_ab.txt: a scratch-write flush instead costs 1-2 us
+per step through TLB misses).  ``value`` = elements of all ranks / max over ranks
+of the region time.
 
 Roofline (``roofline``): ``achieved`` = algorithmic bytes per launch (SURVEY
 §8d: N/2 packed + 2N out + nb absmax + 4*min(n2, m*G) nested absmax) / mean
@@ -84,7 +88,9 @@ def parse_args(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
     ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = enough for >= 1 GiB)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-flush", action="store_true", help="skip the Infinity-Cache flush before timing")
+    ap.add_argument("--lead", default="replay", choices=["replay", "spin", "none"],
+                    help="device work enqueued just ahead of the start event (A/B)")
+    ap.add_argument("--flush", action="store_true", help="512 MiB Infinity-Cache flush before timing (A/B only)")
     ap.add_argument("--tile-dwords", type=int, default=4)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=1)
@@ -263,6 +269,15 @@ def main():
     P = args.sets or max(2, -(-MIN_FOOTPRINT // max(1, step_bytes)))
     if cpu:
         P = args.sets or 2
+    elif not args.sets:
+        # across the boundary between two replays set 0 is reused after
+        # K - P*floor((K-1)/P) steps (K when P >= K): keep that >= 256 MiB so no set
+        # is still in the Infinity Cache when the timed replay reaches it
+        def reuse(p):
+            return args.steps if p >= args.steps else args.steps - p * ((args.steps - 1) // p)
+
+        while P < args.steps and reuse(P) * step_bytes < (256 << 20):
+            P += 1
     all_mats = [rank_matrices(args, r, world) for r in range(world)]
     t_setup = time.perf_counter()
     if rank == 0:
@@ -362,9 +377,10 @@ def main():
             log(f"[rank {rank}] hipGraph capture failed ({e}); timing eager launches")
             graph = None
             torch.cuda.synchronize()
-    if not cpu and not args.no_flush:
-        # evict what the untimed pass left in the Infinity Cache (its last sets are
-        # the timed pass's first ones when K is not a multiple of P)
+    if not cpu and args.flush:
+        # optional: evict the Infinity Cache with a 512 MiB scratch write (measured:
+        # costs 1-2 us per step afterwards -- the new allocation's mappings evict the
+        # GPU TLBs -- so the buffer-set rule above is the default hygiene instead)
         scratch = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
         scratch.fill_(1)
         torch.cuda.synchronize()
@@ -383,6 +399,14 @@ def main():
         main_stream = torch.cuda.current_stream(dev)
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
+        if graph is not None:
+            if args.lead == "replay":
+                # one more untimed replay enqueued right ahead of the start event: the
+                # timed steps follow warm steps back to back (as in a steady stream of
+                # work) and the host's submission of the timed replay hides behind it
+                graph.replay()
+            elif args.lead == "spin":
+                torch.cuda._sleep(100_000)  # ~50 us spin: hides only the host's submission
         ev0.record(main_stream)
         if graph is not None:
             graph.replay()
@@ -452,7 +476,7 @@ def main():
             "buffer_sets": P, "launch": "hipGraph" if graph is not None else ("host loop" if cpu else "eager"),
             "tile_dwords": args.tile_dwords, "blocks_per_cu": args.blocks_per_cu, "nontemporal": args.nontemporal,
             "flags": args.flags, "parallelism": f"shard{world} (independent matrices)",
-            "cache_flush_before_timing": not cpu and not args.no_flush,
+            "cache_flush_before_timing": bool(not cpu and args.flush), "lead": args.lead,
             "quant_state_broadcast_ms": round(bcast_ms, 3), "dist_backend": dist_backend if world > 1 else None,
         },
         "roofline": None if cpu else {

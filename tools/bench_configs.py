@@ -18,7 +18,11 @@ bnb  4096x4096 NF4->bf16 with bitsandbytes semantics (nf4_dequant_bnb: code2[A1]
 
 Every line: elements/s and algorithmic GB/s (SURVEY §8d bytes) vs the 8 TB/s
 peak; timing = HIP events around the whole pass on the launch stream (c3/c3b: the
-pass captured in a hipGraph, the eager figure alongside).
+pass captured in a hipGraph, the eager figure alongside).  After timing, every
+output the timed launches wrote is compared bit for bit with the C oracle
+(``verified`` / ``verified_matrices`` in the line; a mismatch fails the run); the
+oracle is pinned to the reference fallback at each of these shapes
+(tests/golden/manifest.json C2/C3/C3b/C4/C5 digests).
 """
 from __future__ import annotations
 
@@ -28,11 +32,37 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
 from nf4_triton_dequantization_amd import _lib  # noqa: E402
+import nf4_oracle as O  # noqa: E402  -- the checker of the timed outputs
+
+_CORACLE = None
+
+
+def verify(ws, code, bnb_code2=None, bnb_offset=0.0):
+    """Every (q, a1, a2, out) output vs the C oracle on the same inputs; raises on a mismatch."""
+    global _CORACLE
+    if _CORACLE is None:
+        _CORACLE = O.COracle()
+        _CORACLE.set_threads(16)
+    ocode = {_lib.F16: O.F16, _lib.BF16: O.BF16, _lib.F32: O.F32}[code]
+    for i, (q, a1, a2, o) in enumerate(ws):
+        m, n = o.shape
+        hq, h1, h2 = q.cpu().numpy(), a1.cpu().numpy(), a2.cpu().numpy()
+        if bnb_code2 is None:
+            want = _CORACLE.dequant_ref(hq, h1, h2, m, n, ocode)
+        else:
+            want = _CORACLE.dequant_bnb(hq, h1, bnb_code2, h2, bnb_offset, m * n, ocode).reshape(m, n)
+        wt = torch.from_numpy(want.view(np.int32 if code == _lib.F32 else np.int16)).to(o.device)
+        got = o.view(torch.int32 if code == _lib.F32 else torch.int16)
+        if not torch.equal(got, wt):
+            raise AssertionError(f"output {i} ({m}x{n}) differs from the oracle")
+    return len(ws)
 
 PEAK = 8.0e12
 LLAMA3_8B = [(4096, 4096), (1024, 4096), (1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 14336)]
@@ -94,7 +124,8 @@ def run_model(name, shapes, layers, reps, dev):
     elems = sum(o.numel() for *_, o in ws)
     byt = sum(alg_bytes(o.shape[0], o.shape[1], 2) for *_, o in ws)
     launches = -(-len(ws) // _lib.BATCH_MAX)
-    return {"config": name, "matrices": len(ws), "launches": launches, "elements": elems, "seconds": t,
+    checked = verify(ws, _lib.BF16)
+    return {"config": name, "verified": True, "verified_matrices": checked, "matrices": len(ws), "launches": launches, "elements": elems, "seconds": t,
             "elements_per_s": elems / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK,
             "timing": "hipGraph replay of the pass", "eager_seconds": te, "eager_frac": byt / te / PEAK}
 
@@ -114,7 +145,8 @@ def run_single(name, m, n, dt, code, reps, dev, sets=16, steps=64):
     t = timed(graph.replay, reps) / steps
     ob = torch.empty((), dtype=dt).element_size()
     byt = alg_bytes(m, n, ob)
-    return {"config": name, "m": m, "n": n, "out_dtype": str(dt).replace("torch.", ""), "us_per_launch": t * 1e6,
+    checked = verify(ws[:min(sets, steps)], code)
+    return {"config": name, "verified": True, "verified_matrices": checked, "m": m, "n": n, "out_dtype": str(dt).replace("torch.", ""), "us_per_launch": t * 1e6,
             "elements_per_s": m * n / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK}
 
 
@@ -136,7 +168,8 @@ def run_bnb(name, m, n, reps, dev, sets=16, steps=64):
     t = timed(graph.replay, reps) / steps
     nb = numel // 64
     byt = numel // 2 + 2 * numel + nb + 4 * ((nb + 255) // 256) + 1024
-    return {"config": name, "m": m, "n": n, "out_dtype": "bfloat16", "us_per_launch": t * 1e6,
+    checked = verify(ws[:min(sets, steps)], _lib.BF16, bnb_code2=code2.cpu().numpy(), bnb_offset=np.float32(0.0123))
+    return {"config": name, "verified": True, "verified_matrices": checked, "m": m, "n": n, "out_dtype": "bfloat16", "us_per_launch": t * 1e6,
             "elements_per_s": numel / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK}
 
 

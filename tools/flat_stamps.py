@@ -39,8 +39,11 @@ def main():
     ap.add_argument("--tile-dwords", type=int, default=4)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     args = ap.parse_args()
-    _lib.LIB_PATH = os.path.join(REPO, "tools", "_build", "libnf4dq_stamps.so")
-    L = _lib.lib()
+    # the diagnostic build beside the product one (the package import already
+    # loaded libnf4dq.so); only the two entry points used here are bound
+    L = ctypes.CDLL(os.path.join(REPO, "tools", "_build", "libnf4dq_stamps.so"))
+    L.nf4_dequant_ref_cfg.restype = ctypes.c_int
+    L.nf4_dequant_ref_cfg.argtypes = _lib.SIGNATURES["nf4_dequant_ref_cfg"][1]
     L.nf4_dbg_set_stamps.argtypes = [ctypes.c_void_p]
     L.nf4_dbg_set_stamps.restype = None
     dev = torch.device("cuda", 0)

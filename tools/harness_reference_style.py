@@ -135,8 +135,18 @@ def main():
         torch.empty((4096, 4096), dtype=torch.bfloat16, device="cuda")
     empty_us = (time.perf_counter() - t0) * 1e6 / n
     torch.cuda.synchronize()
+    # and one minimal torch kernel launch (an in-place add on 1 element): the host cost
+    # of any single kernel launch from Python on this stack
+    tiny = torch.zeros(1, device="cuda")
+    torch.cuda._sleep(200_000_000)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        tiny.add_(1.0)
+    launch_us = (time.perf_counter() - t0) * 1e6 / n
+    torch.cuda.synchronize()
     print(json.dumps({"reference_style_total_seconds": total, "api_host_us_per_call": host_us,
-                      "api_host_us_per_call_plain_tensors": duck_us, "torch_empty_us": empty_us}), flush=True)
+                      "api_host_us_per_call_plain_tensors": duck_us, "torch_empty_us": empty_us,
+                      "torch_min_kernel_launch_us": launch_us}), flush=True)
 
 
 if __name__ == "__main__":
