@@ -20,9 +20,9 @@ WORLD_SIZE must equal N.
 
 Timed region (``value``): K steps captured once into a hipGraph and replayed,
 bracketed by barrier + synchronize on both sides, HIP events on the launch
-stream around the replay; one more untimed replay is enqueued right ahead of the
-start event (no host sync in between), so the timed steps follow warm steps back
-to back and the host's submission latency is hidden behind it.  Step i uses buffer set i % P; P is chosen so
+stream around the replay (``--lead replay|spin`` enqueue untimed device work just
+ahead of the start event; A/B in profiles/r02/bench_lead_ab.txt: within noise,
+so the default is none).  Step i uses buffer set i % P; P is chosen so
 each rank's sets span >= 1 GiB (>> the 256 MiB Infinity Cache) and so that a set
 is reused >= 256 MiB of traffic later across the untimed -> timed replay
 boundary (profiles/r02/bench_ab.txt: a scratch-write flush instead costs 1-2 us
@@ -88,7 +88,7 @@ def parse_args(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
     ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = enough for >= 1 GiB)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--lead", default="replay", choices=["replay", "spin", "none"],
+    ap.add_argument("--lead", default="none", choices=["replay", "spin", "none"],
                     help="device work enqueued just ahead of the start event (A/B)")
     ap.add_argument("--flush", action="store_true", help="512 MiB Infinity-Cache flush before timing (A/B only)")
     ap.add_argument("--tile-dwords", type=int, default=4)
