@@ -175,6 +175,12 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
 #define NF4DQ_GEMM_K128 1
 #define NF4DQ_GEMM_STREAM 2
 #define NF4DQ_GEMM_PERSIST 3
+/* NF4DQ_GEMM_XS: shared-activation kernel (any M <= 32, K % 128 == 0): a
+ * workgroup of `waves` (4/8) waves owns one 16-column strip per wave over a K
+ * slice of `depth` (2/4/8) 128-deep chunks, the x slice staged once in LDS and
+ * every weight chunk in flight at once; ksplit must equal ceil(K/128 / depth);
+ * strips 0 or 1. */
+#define NF4DQ_GEMM_XS 4
 typedef struct nf4_gemm_cfg {
     int32_t kernel;
     int32_t waves;

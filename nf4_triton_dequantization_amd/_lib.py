@@ -14,7 +14,9 @@ import threading
 import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libnf4dq.so")
+# NF4DQ_LIB_PATH: load a diagnostic build of the same library instead (tools/Makefile);
+# unset in every product / test / bench run
+LIB_PATH = os.environ.get("NF4DQ_LIB_PATH") or os.path.join(_HERE, "_lib", "libnf4dq.so")
 EXT_PATH = os.path.join(_HERE, "_lib", "nf4ext.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nf4_dequant.h")
 
@@ -63,6 +65,7 @@ CFG_NT_LOADS = 1
 GEMM_K128 = 1
 GEMM_STREAM = 2
 GEMM_PERSIST = 3
+GEMM_XS = 4
 
 
 GEMM_GROUP_MAX = 8

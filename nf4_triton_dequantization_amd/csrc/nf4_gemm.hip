@@ -39,6 +39,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kAuxSc1 = 16;  // write-through stores / L2-bypassing loads (cross-XCD hand-off)
 constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads return 0, stores drop
 
+// Diagnostic builds of the shared-activation kernel (tools/Makefile xsdbg): 1 = no
+// LUT reads in the dequant, 2 = no x fragment reads from LDS.
+#ifndef NF4_XS_DEBUG
+#define NF4_XS_DEBUG 0
+#endif
+
+
 // The last arriver's split-K sum for one column group of KCOLS columns: slab
 // [ksplit][M][ld] fp32 (sc1-written by every slice), columns col0.. of the
 // slab -> y[m][ycol0 ..] (row stride yld), slices added in slice order (bitwise
@@ -344,6 +351,178 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     if (!last) return;
     splitk_reduce<DT, 16u * NT>(rs, A.ksplit, A.M, A.ncols, Mt.col_begin + cgl * 16u * NT, Mt.y, Mt.N, cgl * 16u * NT,
                                 lane);
+}
+
+// ---------------------------------------------------------------------------
+// Shared-activation decode kernel (K % 128 == 0; built for 16 < M <= 32).  The
+// 128-deep kernel's waves split K over the same columns, so every workgroup
+// streams the whole x[M][K] through its vector-memory path and a wave can hold
+// only one or two weight chunks in registers next to its x fragments -- at
+// M = 32 that left 7 waves per CU with ~28 KB of weight bytes in flight and the
+// address FIFO saturated (profiles/r01/pmc_gemm_m32_14336x4096.txt).  Here a
+// workgroup owns WV 16-column strips (one per wave) over one K slice of KC
+// 128-deep chunks:
+//  * the slice of x (M x KC*128 bf16, rows padded 16 B so consecutive rows
+//    start 4 banks apart) is loaded ONCE per workgroup and read by all WV
+//    waves from LDS (ds_read_b128), so x costs 1/WV of the vector-memory
+//    instructions and no registers between chunks;
+//  * each wave issues ALL KC of its weight chunks (16 B per lane each) before
+//    it waits on anything, so a CU with two workgroups of 8 waves keeps
+//    16 x KC KiB of weight bytes in flight;
+//  * the block scales of the workgroup's 16 WV rows x 2 KC blocks are built once
+//    in LDS from gathers with the reference's wrap (any nb / n2);
+//  * K slices over workgroups meet in the fp32 slab: one ticket per strip, the
+//    last arriver sums the slices in slice order (bitwise reproducible).
+// Same k permutation, dequant and MFMA step as the 128-deep kernel (chunk_mma).
+template <int DT, int MT, int KC, int WV>
+__global__ __launch_bounds__(64 * WV, 4) void nf4_gemm_xs_kernel(const GemmArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr uint32_t XS = KC * 256u + 16u;                 // LDS bytes per staged x row
+    constexpr uint32_t kScl = 16u * MT * XS;                 // scale table [16 WV rows][2 KC blocks]
+    constexpr uint32_t kLut = kScl + 16u * WV * 2u * KC * 4u;
+    float* scl = reinterpret_cast<float*>(smem + kScl);
+    float* lut = reinterpret_cast<float*>(smem + kLut);
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t nl = lane & 15u, kh = lane >> 4;
+    const uint32_t cg = blockIdx.x % A.col_groups;  // group of WV strips, launch-wide
+    const uint32_t ks = blockIdx.x / A.col_groups;  // K slice
+    uint32_t mi = 0;                                // the weight this workgroup works on (uniform scan)
+    for (uint32_t i = 1; i < A.nmat; ++i) mi = cg >= A.mat[i].cg_begin ? i : mi;
+    const K128Mat& Mt = A.mat[mi];
+    const uint32_t strip0 = (cg - Mt.cg_begin) * (uint32_t)WV;  // first strip of this workgroup in the weight
+    const uint32_t strip = strip0 + wave;
+    const bool live = strip < (Mt.N >> 4);          // wave-uniform (a weight's last group may be partial)
+    const uint32_t row = strip * 16u + nl;
+    const uint32_t c0s = ks * (uint32_t)KC;
+    const uint32_t c0 = c0s < A.chunks ? c0s : A.chunks;  // an empty last slice: c1 == c0
+    const uint32_t c1 = c0 + KC < A.chunks ? c0 + KC : A.chunks;
+    const uint32_t kc = c1 - c0;
+
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
+
+    // 1. the x slice (rows >= M and chunks past c1 read as zeros: out-of-range offsets)
+    constexpr uint32_t kPpr = KC * 16u;              // 16-byte pieces per row
+    constexpr uint32_t kPieces = 16u * MT * kPpr;
+    constexpr int XR = (int)((kPieces + 64u * WV - 1u) / (64u * WV));
+    u32x4 xv[XR];
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+        const uint32_t p = tid + (uint32_t)i * 64u * WV;
+        const uint32_t r = p / kPpr, q = p % kPpr;
+        const bool ok = p < kPieces && r < A.M && q < kc * 16u;
+        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? (r * A.K + c0 * kChunkK) * 2u + q * 16u : kOob, 0, 0);
+    }
+    // 2. the block-scale gathers of the workgroup's rows (reference wrap, :173-186)
+    constexpr uint32_t kSclN = 16u * WV * 2u * KC;
+    constexpr int SR = (int)((kSclN + 64u * WV - 1u) / (64u * WV));
+    uint32_t qa[SR];
+    float qb[SR];
+#pragma unroll
+    for (int i = 0; i < SR; ++i) {
+        const uint32_t e = tid + (uint32_t)i * 64u * WV;
+        const uint32_t rr = e / (2u * KC), j = e % (2u * KC);
+        const uint32_t r = strip0 * 16u + rr, b = 2u * c0 + j;
+        const bool ok = e < kSclN && r < Mt.N && j < 2u * kc;
+        qa[i] = ok ? Mt.a1[fmodu(r * A.bpr + b, Mt.nb)] : 0u;
+        qb[i] = ok ? Mt.a2[fmodu(r * A.groups + (b >> 2), Mt.n2)] : 0.0f;
+    }
+    // 3. every weight chunk of this wave, all in flight before the first wait
+    u32x4 w[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        const uint32_t c = c0 + (uint32_t)j;
+        w[j] = __builtin_amdgcn_raw_buffer_load_b128(
+            rw, live && (uint32_t)j < kc ? row * (A.K >> 1) + ((c * kChunkK + 32u * kh) >> 1) : kOob, 0, 0);
+    }
+    // 4. tables and the staged slice (waits for x and the scale gathers only), one barrier
+    write_lut(lut);
+#pragma unroll
+    for (int i = 0; i < SR; ++i) {
+        const uint32_t e = tid + (uint32_t)i * 64u * WV;
+        if (e < kSclN) scl[e] = ((float)qa[i] / 127.0f) * qb[i];  // IEEE division, fp32 multiply (:45)
+    }
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+        const uint32_t p = tid + (uint32_t)i * 64u * WV;
+        if (p < kPieces) *reinterpret_cast<u32x4*>(smem + (p / kPpr) * XS + (p % kPpr) * 16u) = xv[i];
+    }
+    __syncthreads();
+
+    // 5. the chunks: x fragments from LDS, the wave's weights from registers
+    f32x4 acc[MT][1];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint32_t srow = (wave * 16u + nl) * 2u * KC + (kh >> 1);
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        if ((uint32_t)j < kc) {  // uniform
+            Chunk<MT, 1> ch;
+            ch.w[0] = w[j];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#if NF4_XS_DEBUG == 2
+                    ch.x[mt][s] = u32x4{(uint32_t)j, nl, kh, (uint32_t)s};  // diagnostic: no x reads
+#else
+                    ch.x[mt][s] = *reinterpret_cast<const u32x4*>(smem + (16u * mt + nl) * XS + (uint32_t)j * 256u +
+                                                                 64u * kh + 16u * s);
+#endif
+            const float scs[1] = {scl[srow + 2u * (uint32_t)j]};
+#if NF4_XS_DEBUG == 1
+            // diagnostic: no LUT reads (the weight bits go straight into the MMA)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    const u32x4 bw = {ch.w[0][s4], ch.w[0][s4] ^ __float_as_uint(scs[0]), ch.w[0][s4] >> 1, ch.w[0][s4] << 1};
+                    acc[mt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8, ch.x[mt][s4]), __builtin_bit_cast(bf16x8, bw), acc[mt][0], 0, 0, 0);
+                }
+#else
+            chunk_mma<DT, MT, 1>(ch, lut, scs, acc);
+#endif
+        }
+    }
+    if (!live) return;
+
+    // acc[mt][0][r] = Y[16 mt + 4 kh + r][row]
+    if (A.ksplit == 1) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t m = 16u * mt + 4u * kh + r;
+                if (m < A.M) store_y<DT>(Mt.y, m * Mt.N + row, acc[mt][0][r]);
+            }
+        return;
+    }
+    // split-K: this wave's strip slice to the slab (write-through), drained; one
+    // ticket per strip; the last arriver sums the slices in slice order
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)A.slab, 0, A.ksplit * A.M * A.ncols * 4u, kRsrcFlags);
+    const uint32_t scol = Mt.col_begin + row;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t m = 16u * mt + 4u * kh + r;
+            const uint32_t off = m < A.M ? ((ks * A.M + m) * A.ncols + scol) * 4u : kOob;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][0][r]), rs, off, 0, kAuxSc1);
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partials are out: the hand-off
+    const uint32_t ctr = (Mt.col_begin >> 4) + strip;
+    uint32_t last = 0;
+    if (lane == 0) {
+        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[ctr], 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        last = ticket == A.ksplit - 1u;
+        if (last) __hip_atomic_store(&A.counters[ctr], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last = __builtin_amdgcn_readfirstlane(last);
+    if (!last) return;
+    splitk_reduce<DT, 16u>(rs, A.ksplit, A.M, A.ncols, Mt.col_begin + strip * 16u, Mt.y, Mt.N, strip * 16u, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1108,6 +1287,13 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
         if (c.ksplit < 1 || c.ksplit > K / kSChunkK) return false;
         return stream_fits(M, K, c);
     }
+    if (c.kernel == NF4DQ_GEMM_XS) {
+        if (c.waves != 4 && c.waves != 8) return false;
+        if (c.depth != 2 && c.depth != 4 && c.depth != 8) return false;
+        if (c.strips != 0 && c.strips != 1) return false;
+        const int64_t chunks = K / kChunkK;
+        return c.ksplit == (chunks + c.depth - 1) / c.depth && c.ksplit <= 256;
+    }
     if (c.kernel != NF4DQ_GEMM_K128) return false;
     if (c.waves != 4 && c.waves != 8) return false;
     if (c.strips != 0 && c.strips != 1 && c.strips != 2 && c.strips != 4) return false;  // strips per wave
@@ -1349,6 +1535,85 @@ static int launch_persist(const HostMat* mats, int count, const void* x, int64_t
 
 // One launch of the 128-deep kernel over `count` weights sharing x (shapes and
 // cfg validated; workspace = counters + ksplit * M * sum(N) fp32 when ksplit > 1).
+// LDS bytes of the shared-activation kernel: x slice (16 MT rows) + scale table + LUT.
+static uint32_t xs_lds_bytes(int64_t M, int kc, int waves) {
+    const uint32_t mt = M > 16 ? 2u : 1u;
+    return 16u * mt * ((uint32_t)kc * 256u + 16u) + 16u * (uint32_t)waves * 2u * (uint32_t)kc * 4u + 64u;
+}
+
+// One launch of the shared-activation kernel over `count` weights sharing x (shapes
+// and cfg validated: cfg.depth = KC chunks per slice, cfg.ksplit = ceil(chunks / KC)).
+static int launch_xs(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
+                     const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st) {
+    const uint32_t ks = (uint32_t)cfg.ksplit;
+    GemmArgs A{};
+    A.nmat = (uint32_t)count;
+    A.x = x;
+    A.counters = reinterpret_cast<uint32_t*>(workspace);
+    A.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    A.M = (uint32_t)M;
+    A.K = (uint32_t)K;
+    A.ksplit = ks;
+    A.chunks = (uint32_t)(K / kChunkK);
+    A.chunks_per_split = (uint32_t)cfg.depth;
+    A.bpr = (uint32_t)(K / 64);
+    A.groups = (A.bpr + 3) / 4;
+    const uint32_t cols_per_group = 16u * (uint32_t)cfg.waves;
+    uint32_t cgs = 0, cols = 0;
+    for (int i = 0; i < count; ++i) {
+        const HostMat& h = mats[i];
+        K128Mat& m = A.mat[i];
+        m.packed = h.packed;
+        m.a1 = h.a1;
+        m.a2 = h.a2;
+        m.y = h.y;
+        m.N = (uint32_t)h.N;
+        m.cg_begin = cgs;
+        m.col_begin = cols;
+        m.nb = make_fastdiv((uint32_t)(h.nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : h.nb));
+        m.n2 = make_fastdiv((uint32_t)(h.n2 > (int64_t(1) << 31) ? (int64_t(1) << 31) : h.n2));
+        cgs += ((uint32_t)h.N + cols_per_group - 1u) / cols_per_group;
+        cols += (uint32_t)h.N;
+    }
+    A.col_groups = cgs;
+    A.ncols = cols;
+    const dim3 grid(cgs * ks), block(64 * cfg.waves);
+    const uint32_t lds = xs_lds_bytes(M, cfg.depth, cfg.waves);
+#define NF4_X1(DT_, MT_, KC_, W_)                                                                                   \
+    do {                                                                                                            \
+        static bool attr_ = false; /* dynamic LDS above 64 KiB needs the opt-in */                                  \
+        if (!attr_) {                                                                                               \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_xs_kernel<DT_, MT_, KC_, W_>),        \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);                  \
+            attr_ = true;                                                                                           \
+        }                                                                                                           \
+        hipLaunchKernelGGL((nf4_gemm_xs_kernel<DT_, MT_, KC_, W_>), grid, block, lds, st, A);                       \
+    } while (0)
+#define NF4_XW(DT_, MT_, KC_)                          \
+    do {                                               \
+        if (cfg.waves == 8) NF4_X1(DT_, MT_, KC_, 8);  \
+        else NF4_X1(DT_, MT_, KC_, 4);                 \
+    } while (0)
+#define NF4_XK(DT_, MT_)                              \
+    do {                                              \
+        if (cfg.depth == 8) NF4_XW(DT_, MT_, 8);      \
+        else if (cfg.depth == 4) NF4_XW(DT_, MT_, 4); \
+        else NF4_XW(DT_, MT_, 2);                     \
+    } while (0)
+#define NF4_XM(DT_)                        \
+    do {                                   \
+        if (M > 16) NF4_XK(DT_, 2);        \
+        else NF4_XK(DT_, 1);               \
+    } while (0)
+    if (dtype == NF4DQ_BF16) NF4_XM(NF4DQ_BF16);
+    else NF4_XM(NF4DQ_F16);
+#undef NF4_XM
+#undef NF4_XK
+#undef NF4_XW
+#undef NF4_X1
+    return hip_rc2(hipGetLastError());
+}
+
 static int launch_k128(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
                        const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st) {
     const uint32_t ks = (uint32_t)cfg.ksplit;
@@ -1464,6 +1729,7 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
         return launch_stream(&h, 1, x, M, K, dtype, cfg, workspace, st);
     }
     const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
+    if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(&h, 1, x, M, K, dtype, cfg, workspace, st);
     return launch_k128(&h, 1, x, M, K, dtype, cfg, workspace, st);
 }
 
@@ -1494,7 +1760,7 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
     for (int i = 0; i < count; ++i) {
         // an empty weight cannot own strip groups (the 128-deep kernel numbers
         // column groups per weight: an empty one simply owns none)
-        if (mats[i].N == 0 && cfg.kernel != NF4DQ_GEMM_K128) return NF4DQ_ERR_SHAPE;
+        if (mats[i].N == 0 && cfg.kernel != NF4DQ_GEMM_K128 && cfg.kernel != NF4DQ_GEMM_XS) return NF4DQ_ERR_SHAPE;
         if (mats[i].N == 0) continue;
         if (!valid_gemm_cfg(cfg, M, mats[i].N, K)) return NF4DQ_ERR_ARG;
         if (mats[i].packed_len >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
@@ -1507,6 +1773,7 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
         h[i] = HostMat{mats[i].packed, mats[i].packed_len, mats[i].absmax_q, mats[i].nb, mats[i].absmax2,
                        mats[i].n2, mats[i].y, mats[i].N};
     if (cfg.kernel == NF4DQ_GEMM_K128) return launch_k128(h, count, x, M, K, dtype, cfg, workspace, st);
+    if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
         const int rc = launch_persist(h, count, x, M, K, dtype, cfg, workspace, st);
         if ((rc != NF4DQ_ERR_ARG && rc != NF4DQ_ERR_TOO_LARGE) || cfgp) return rc;

@@ -448,3 +448,83 @@ def test_k128_slices_starting_past_the_end(coracle, gpu, ks):
     assert rc == 0, rc
     torch.cuda.synchronize()
     _check(y, xb, Ws[0], "bf16")
+
+
+def _xs_cfg(_lib, K, waves, kc):
+    chunks = K // 128
+    return _lib.GemmCfg(_lib.GEMM_XS, waves, kc, -(-chunks // kc), 1)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,N,K", [(32, 1024, 4096), (17, 192, 1280), (24, 448, 384), (1, 64, 128), (9, 320, 2304),
+                                   (32, 64, 11008), (30, 4160, 1024)])
+def test_shared_activation_kernel_vs_oracle(coracle, gpu, dt, M, N, K):
+    """NF4DQ_GEMM_XS, every (waves, chunks per slice) it accepts: full slices, a
+    partial last slice (K/128 not a multiple), ksplit 1 (no slab) and > 1, a
+    partial last strip group (N not a multiple of 16 x waves), M rows padded."""
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    packed, a1, a2 = O.make_inputs(N, K, seed=N + 3 * K + M, a2_kind="normal")
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16)
+    t = (torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu))
+    xt, xb = _x_bits(M, K, dt, seed=M * 7 + 3)
+    x = xt.to(gpu)
+    code = _lib.BF16 if dt == "bf16" else _lib.F16
+    y = torch.empty((M, N), dtype=x.dtype, device=gpu)
+    ran = 0
+    for waves in (4, 8):
+        for kc in (2, 4, 8):
+            cfg = _xs_cfg(_lib, K, waves, kc)
+            for _ in range(2):  # twice: the tickets the first call left at 0 are reused
+                y.fill_(float("nan"))
+                rc = _gemm_cfg_call(L, _lib, x, t, y, code, N, K, cfg)
+                assert rc == 0, (waves, kc, rc)
+                _check(y, xb, W, dt)
+            ran += 1
+    assert ran == 6
+    bad = _lib.GemmCfg(_lib.GEMM_XS, 8, 4, -(-(K // 128) // 4) + 1, 1)  # ksplit must be ceil(chunks / depth)
+    assert _gemm_cfg_call(L, _lib, x, t, y, code, N, K, bad) == _lib.ERR_ARG
+
+
+@pytest.mark.parametrize("wrap", [False, True])
+def test_shared_activation_kernel_grouped(coracle, gpu, wrap):
+    """One grouped launch of the shared-activation kernel (q/k/v-like); `wrap` adds a
+    weight whose absmax / nested absmax wrap inside rows (the scale table gathers
+    with the reference's modular indices, so no fallback is needed)."""
+    import ctypes
+
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    M, K = 32, 2048
+    Ns = (1024, 256, 320) + ((128,) if wrap else ())
+    mats = (_lib.GemmMat * len(Ns))()
+    ys, keep, Ws = [], [], []
+    for i, N in enumerate(Ns):
+        if wrap and i == 3:
+            packed, a1, a2 = O.golden_case_inputs(N, K, 5, {"nb": 37, "n2": 5})[:3]
+        else:
+            packed, a1, a2 = O.make_inputs(N, K, seed=5 * N + i, a2_kind="normal")
+        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16))
+        tt = [torch.from_numpy(v).to(gpu) for v in (packed, a1, a2)]
+        keep.append(tt)
+        y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+        ys.append(y)
+        mats[i] = _lib.GemmMat(tt[0].data_ptr(), tt[0].numel(), tt[1].data_ptr(), tt[1].numel(), tt[2].data_ptr(),
+                               tt[2].numel(), y.data_ptr(), N)
+    xt, xb = _x_bits(M, K, "bf16", seed=61)
+    x = xt.to(gpu)
+    for waves, kc in ((8, 4), (4, 8), (8, 2)):
+        c = _xs_cfg(_lib, K, waves, kc)
+        wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, mats, len(Ns), ctypes.byref(c))
+        ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=gpu)
+        for y in ys:
+            y.fill_(float("nan"))
+        rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, mats, len(Ns), _lib.BF16, ws.data_ptr(), wsz,
+                                    ctypes.byref(c), torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+        for y, W in zip(ys, Ws):
+            _check(y, xb, W, "bf16")
+        assert int(ws[:65536].view(torch.int32).abs().sum()) == 0  # tickets back at 0

@@ -52,7 +52,8 @@ def main():
     ap.add_argument("--ms", default="1,16,32")
     ap.add_argument("--budget-mb", type=int, default=768, help="packed weight bytes per shape")
     ap.add_argument("--shapes", default="", help="N,K;N,K;... (default: the Llama-3-8B list)")
-    ap.add_argument("--kernels", default="1,2,3", help="kernel ids to sweep (1 K128, 2 stream, 3 persist)")
+    ap.add_argument("--kernels", default="1,2,3,4",
+                    help="kernel ids to sweep (1 K128, 2 stream, 3 persist, 4 shared-activation)")
     args = ap.parse_args()
     shapes = [tuple(int(v) for v in s.split(",")) for s in args.shapes.split(";")] if args.shapes else SHAPES
     kern = {int(v) for v in args.kernels.split(",")}
@@ -87,6 +88,9 @@ def main():
                     for strips in (1, 2, 4):  # K128: strips per wave
                         for ks in (1, 2, 4, 8):
                             cfgs.append(_lib.GemmCfg(_lib.GEMM_K128, waves, depth, ks, strips))
+            for waves in (4, 8):
+                for kc in (2, 4, 8):  # shared-activation kernel: chunks per K slice; ksplit follows
+                    cfgs.append(_lib.GemmCfg(_lib.GEMM_XS, waves, kc, -(-(k // 128) // kc), 1))
             cfgs = [c for c in cfgs if c.kernel in kern]
             for cfg in cfgs:
                 wsz = L.nf4_gemm_workspace_bytes_cfg(M, n, k, ctypes.byref(cfg))
