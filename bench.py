@@ -88,6 +88,9 @@ def parse_args(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
     ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = enough for >= 1 GiB)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--events", default="stream", choices=["stream", "graph"],
+                    help="timing events around the replay on the stream, or recorded as graph nodes around "
+                         "the K launches (A/B)")
     ap.add_argument("--lead", default="none", choices=["replay", "spin", "none"],
                     help="device work enqueued just ahead of the start event (A/B)")
     ap.add_argument("--flush", action="store_true", help="512 MiB Infinity-Cache flush before timing (A/B only)")
@@ -365,12 +368,20 @@ def main():
         launch(w)
     sync()
     graph = None
+    gev = None  # (start, end) event-record nodes inside the graph (--events graph)
     if not cpu and not args.no_graph:
         try:
             graph = torch.cuda.CUDAGraph()
+            if args.events == "graph":
+                gev = (torch.cuda.Event(enable_timing=True, external=True),
+                       torch.cuda.Event(enable_timing=True, external=True))
             with torch.cuda.graph(graph):
+                if gev is not None:
+                    gev[0].record()
                 for i in range(args.steps):
                     launch(i)
+                if gev is not None:
+                    gev[1].record()
             graph.replay()  # upload + one untimed pass
             torch.cuda.synchronize()
         except Exception as e:  # capture unsupported -> eager issue, reported in config
@@ -415,7 +426,7 @@ def main():
                 launch(i)
         ev1.record(main_stream)
         torch.cuda.synchronize()
-        t_ms = ev0.elapsed_time(ev1)
+        t_ms = ev0.elapsed_time(ev1) if gev is None else gev[0].elapsed_time(gev[1])
     if world > 1:
         dist.barrier()
     my_ms = t_ms
@@ -477,6 +488,7 @@ def main():
             "tile_dwords": args.tile_dwords, "blocks_per_cu": args.blocks_per_cu, "nontemporal": args.nontemporal,
             "flags": args.flags, "parallelism": f"shard{world} (independent matrices)",
             "cache_flush_before_timing": bool(not cpu and args.flush), "lead": args.lead,
+            "events": "graph nodes" if gev is not None else "stream",
             "quant_state_broadcast_ms": round(bcast_ms, 3), "dist_backend": dist_backend if world > 1 else None,
         },
         "roofline": None if cpu else {

@@ -1230,6 +1230,13 @@ static nf4_gemm_cfg nonpersist_cfg(int64_t M, int64_t N, int64_t K) {
         return k128_cfg(M, N, K, 8, 2, 1, 1);
     }
     if (K >= 8192) return k128_cfg(M, N, K, 8, 1, 4, 4);
+    if (N >= 6144) {
+        // wide launches (gate/up, grouped q/k/v): the shared-activation kernel,
+        // 10-13 % faster than the 128-deep one at M = 24 / 32 (profiles/r02/sweep_gemm_xs.jsonl)
+        const int waves = N >= 12288 ? 8 : 4, kc = N >= 12288 ? 8 : 4;
+        const nf4_gemm_cfg c{NF4DQ_GEMM_XS, waves, kc, (int)((K / kChunkK + kc - 1) / kc), 1};
+        if (valid_gemm_cfg(c, M, N, K)) return c;
+    }
     if (N < 4096) return k128_cfg(M, N, K, 4, 2, 4, 1);
     if (N <= 4096) return k128_cfg(M, N, K, 8, 1, 2, 2);
     if (N < 8192) return k128_cfg(M, N, K, 4, 1, 4, 2);
