@@ -18,16 +18,21 @@ NF4->bf16 (configs[1]).  A *step* is one pass of the hot path over one batch:
 before this process touches the GPU and relays rank 0's line; under a launcher
 WORLD_SIZE must equal N.
 
-Timed region (``value``): K steps captured once into a hipGraph and replayed,
-bracketed by barrier + synchronize on both sides, HIP events on the launch
-stream around the replay (``--lead replay|spin`` enqueue untimed device work just
-ahead of the start event; A/B in profiles/r02/bench_lead_ab.txt: within noise,
-so the default is none).  Step i uses buffer set i % P; P is chosen so
-each rank's sets span >= 1 GiB (>> the 256 MiB Infinity Cache) and so that a set
-is reused >= 256 MiB of traffic later across the untimed -> timed replay
-boundary (profiles/r02/bench_ab.txt: a scratch-write flush instead costs 1-2 us
-per step through TLB misses).  ``value`` = elements of all ranks / max over ranks
-of the region time.
+Timed region (``value``): K steps as K eager launches of the product C-ABI entry
+(``nf4_dequant_ref``, arguments prepared up front), bracketed by barrier +
+synchronize on both sides, HIP events on the launch stream around them.  Ahead of
+the start event sit L = 8 untimed launches of the preceding buffer sets
+(``--lead steps``), so the queue holds real work when timing starts, as in a
+steady stream of weights; before that, one untimed launch per buffer set warms
+the GPU TLB for every set.  ``--launch graph`` captures the K steps into one
+hipGraph instead: on ROCm 7.2 a replay carries a fixed ~7-10 us outside the
+kernels (rocprof: 20 launches span 139 us, the events 149 us), 0.4-0.5 us per
+step at the driver's K = 20 (A/B: profiles/r02/bench_eager_ab.txt).  Step i uses
+buffer set i % P; P is chosen so each rank's sets span >= 1 GiB (>> the 256 MiB
+Infinity Cache) and so that a set is reused >= 256 MiB of traffic later across
+the untimed -> timed boundary (profiles/r02/bench_ab.txt: a scratch-write flush
+instead costs 1-2 us per step through TLB misses).  ``value`` = elements of all
+ranks / max over ranks of the region time.
 
 Roofline (``roofline``): ``achieved`` = algorithmic bytes per launch (SURVEY
 §8d: N/2 packed + 2N out + nb absmax + 4*min(n2, m*G) nested absmax) / mean
@@ -87,12 +92,13 @@ def parse_args(argv=None):
     ap.add_argument("--n", type=int, default=None, help="override the c2 matrix shape (columns)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
     ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = enough for >= 1 GiB)")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--events", default="stream", choices=["stream", "graph"],
-                    help="timing events around the replay on the stream, or recorded as graph nodes around "
-                         "the K launches (A/B)")
-    ap.add_argument("--lead", default="none", choices=["replay", "spin", "none"],
-                    help="device work enqueued just ahead of the start event (A/B)")
+    ap.add_argument("--launch", default="eager", choices=["eager", "graph"],
+                    help="timed steps as eager C-ABI launches (default) or one hipGraph replay")
+    ap.add_argument("--no-graph", action="store_true", help="same as --launch eager (kept for old scripts)")
+    ap.add_argument("--lead", default="auto", choices=["auto", "replay", "spin", "steps", "none"],
+                    help="device work enqueued just ahead of the start event: an untimed graph replay, a spin "
+                         "kernel, or (eager) untimed launches of the preceding buffer sets; auto = steps for "
+                         "eager, none for graph")
     ap.add_argument("--flush", action="store_true", help="512 MiB Infinity-Cache flush before timing (A/B only)")
     ap.add_argument("--tile-dwords", type=int, default=4)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
@@ -226,6 +232,8 @@ def find_traffic(m, n, dtype):
 
 def main():
     args = parse_args()
+    if args.lead == "auto":
+        args.lead = "none" if args.launch == "graph" and not args.no_graph else "steps"
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
@@ -349,6 +357,29 @@ def main():
         if rc:
             raise RuntimeError(f"nf4 dequant launch: {_lib.strerror(rc)}")
 
+    # eager timed loop: one bound C-ABI call per step, arguments prepared up front
+    # (the product entry nf4_dequant_ref when the launch configuration is the default)
+    fast = []
+    if not cpu:
+        sp0 = torch.cuda.current_stream(dev).cuda_stream
+        default_cfg = (args.tile_dwords, args.blocks_per_cu, args.nontemporal, args.flags) == (4, 0, 1, 0)
+        for s_i, row in enumerate(sets):
+            if len(row) == 1:
+                q, a1, a2, out, m, n = row[0]
+                a = (q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(), out.data_ptr(),
+                     code, m, n)
+                fn = L.nf4_dequant_ref if default_cfg else L.nf4_dequant_ref_cfg
+                a = a + ((sp0,) if default_cfg else (cfg_p, sp0))
+            else:
+                fn, a = L.nf4_dequant_ref_batched, (descs[s_i], len(row), code, sp0)
+
+            def call(fn=fn, a=a):
+                rc = fn(*a)
+                if rc:
+                    raise RuntimeError(f"nf4 dequant launch: {_lib.strerror(rc)}")
+            fast.append(call)
+    lead_n = min(8, P)
+
     # correctness sanity of set 0 against the oracle on the first 64 rows of each
     # matrix (the checker; tests/ do the full job)
     launch(0)
@@ -366,22 +397,21 @@ def main():
     # ---- warmup + graph capture ------------------------------------------------------
     for w in range(args.warmup):
         launch(w)
+    if not cpu:
+        # one untimed pass over every buffer set: the first touch of a set's pages
+        # costs +1.5-3 us per 42 MB launch in GPU TLB misses (profiles/r02/bench_lead_ab.txt,
+        # profiles/r02/bench_eager_ab.txt) -- the steady state of a resident weight
+        # set is TLB-warm; the graph path's untimed replay did this implicitly
+        for s_i in range(P):
+            fast[s_i]()
     sync()
     graph = None
-    gev = None  # (start, end) event-record nodes inside the graph (--events graph)
-    if not cpu and not args.no_graph:
+    if not cpu and args.launch == "graph" and not args.no_graph:
         try:
             graph = torch.cuda.CUDAGraph()
-            if args.events == "graph":
-                gev = (torch.cuda.Event(enable_timing=True, external=True),
-                       torch.cuda.Event(enable_timing=True, external=True))
             with torch.cuda.graph(graph):
-                if gev is not None:
-                    gev[0].record()
                 for i in range(args.steps):
                     launch(i)
-                if gev is not None:
-                    gev[1].record()
             graph.replay()  # upload + one untimed pass
             torch.cuda.synchronize()
         except Exception as e:  # capture unsupported -> eager issue, reported in config
@@ -410,23 +440,28 @@ def main():
         main_stream = torch.cuda.current_stream(dev)
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
-        if graph is not None:
-            if args.lead == "replay":
-                # one more untimed replay enqueued right ahead of the start event: the
-                # timed steps follow warm steps back to back (as in a steady stream of
-                # work) and the host's submission of the timed replay hides behind it
-                graph.replay()
-            elif args.lead == "spin":
-                torch.cuda._sleep(100_000)  # ~50 us spin: hides only the host's submission
+        if graph is not None and args.lead == "replay":
+            # one more untimed replay enqueued right ahead of the start event: the
+            # timed steps follow warm steps back to back (as in a steady stream of
+            # work) and the host's submission of the timed replay hides behind it
+            graph.replay()
+        elif args.lead == "spin":
+            torch.cuda._sleep(100_000)  # device spin: hides only the host's submission
+        elif graph is None and args.lead == "steps":
+            # untimed launches of the sets just before the timed ones (steps -L..-1):
+            # the queue holds real work when the start event fires, as in a steady
+            # stream of weights, so host launch latency never idles the GPU
+            for j in range(lead_n):
+                fast[(j - lead_n) % P]()
         ev0.record(main_stream)
         if graph is not None:
             graph.replay()
         else:
             for i in range(args.steps):
-                launch(i)
+                fast[i % P]()
         ev1.record(main_stream)
         torch.cuda.synchronize()
-        t_ms = ev0.elapsed_time(ev1) if gev is None else gev[0].elapsed_time(gev[1])
+        t_ms = ev0.elapsed_time(ev1)
     if world > 1:
         dist.barrier()
     my_ms = t_ms
@@ -488,7 +523,6 @@ def main():
             "tile_dwords": args.tile_dwords, "blocks_per_cu": args.blocks_per_cu, "nontemporal": args.nontemporal,
             "flags": args.flags, "parallelism": f"shard{world} (independent matrices)",
             "cache_flush_before_timing": bool(not cpu and args.flush), "lead": args.lead,
-            "events": "graph nodes" if gev is not None else "stream",
             "quant_state_broadcast_ms": round(bcast_ms, 3), "dist_backend": dist_backend if world > 1 else None,
         },
         "roofline": None if cpu else {
