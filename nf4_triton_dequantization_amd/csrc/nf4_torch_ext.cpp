@@ -13,8 +13,10 @@
 // compute here.
 #include <torch/extension.h>
 
+#include <ATen/hip/EmptyTensor.h>
 #include <ATen/hip/HIPContext.h>
 #include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPFunctions.h>
 
 #include "../../include/nf4_dequant.h"
 
@@ -39,9 +41,16 @@ py::object dequant_ref(const at::Tensor& q, const at::Tensor& a1, const at::Tens
         a1.device() != q.device() || a2.device() != q.device() || a1.numel() == 0 || a2.numel() == 0 || m <= 0 ||
         n <= 0 || code < NF4DQ_F16 || code > NF4DQ_F32)
         return py::none();
-    const c10::DeviceGuard guard(q.device());
-    at::Tensor out = at::empty({m, n}, q.options().dtype(out_type(code)));
-    hipStream_t st = c10::hip::getCurrentHIPStream(q.device().index()).stream();
+    const c10::Device dev = q.device();
+    // a guard only when the weight is not on the current device (the common case
+    // skips the get/set-device pair)
+    std::optional<c10::DeviceGuard> guard;
+    if (dev.index() != c10::hip::current_device()) guard.emplace(dev);
+    // the caching allocator directly (at::detail::empty_cuda), not through the
+    // dispatcher: the output allocation is the largest host cost of the call
+    const int64_t size[2] = {m, n};
+    at::Tensor out(at::detail::empty_cuda(at::IntArrayRef(size, 2), out_type(code), dev, std::nullopt));
+    hipStream_t st = c10::hip::getCurrentHIPStream(dev.index()).stream();
     const int rc = nf4_dequant_ref(q.data_ptr<uint8_t>(), q.numel(), a1.data_ptr<uint8_t>(), a1.numel(),
                                    a2.data_ptr<float>(), a2.numel(), out.data_ptr(), code, m, n, st);
     if (rc != NF4DQ_OK)

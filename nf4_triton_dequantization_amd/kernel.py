@@ -253,8 +253,19 @@ def triton_dequantize_nf4(module) -> torch.Tensor:
     weight = module.weight
     quant_state = weight.quant_state
     absmax32 = quant_state.state2.absmax  # AttributeError when state2 is None, as :151
-    return _dequantize(weight.data, quant_state.absmax, absmax32, quant_state.dtype, int(module.out_features),
-                       int(module.in_features))
+    # `.data` of an nn.Parameter builds a new tensor object per access (~0.8 us);
+    # a Parameter is itself the tensor whose storage `.data` would expose
+    qweight = weight if isinstance(weight, torch.Tensor) else weight.data
+    m, n = int(module.out_features), int(module.in_features)
+    dtype = quant_state.dtype
+    if _EXT is not None:
+        code = _DTYPE_CODE.get(dtype)
+        if code is not None:
+            # common call straight to the tensor-level entry (None = general path)
+            out = _EXT.dequant_ref(qweight, quant_state.absmax, absmax32, m, n, code)
+            if out is not None:
+                return out
+    return _dequantize(weight.data, quant_state.absmax, absmax32, dtype, m, n)
 
 
 def reset_triton_dequantize_state() -> None:
