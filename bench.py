@@ -21,9 +21,13 @@ WORLD_SIZE must equal N.
 Timed region (``value``): K steps as K eager launches of the product C-ABI entry
 (``nf4_dequant_ref``, arguments prepared up front), bracketed by barrier +
 synchronize on both sides, HIP events on the launch stream around them.  Ahead of
-the start event sit L = 8 untimed launches of the preceding buffer sets
-(``--lead steps``), so the queue holds real work when timing starts, as in a
-steady stream of weights; before that, one untimed launch per buffer set warms
+the start event sit L = 8 untimed launches of the preceding buffer sets, so the
+queue holds real work when timing starts, as in a steady stream of weights, and
+ahead of those a device spin that outlasts the host's submission of all L + K
+launches (``--lead spin-steps``): the K kernels then run back to back even when
+a profiler's per-dispatch interception makes the host slower than the GPU (a
+kernel trace without it showed host-bound gaps and per-kernel times 11 % above
+the events' figure); before that, one untimed launch per buffer set warms
 the GPU TLB for every set.  ``--launch graph`` captures the K steps into one
 hipGraph instead: on ROCm 7.2 a replay carries a fixed ~7-10 us outside the
 kernels (rocprof: 20 launches span 139 us, the events 149 us), 0.4-0.5 us per
@@ -95,10 +99,11 @@ def parse_args(argv=None):
     ap.add_argument("--launch", default="eager", choices=["eager", "graph"],
                     help="timed steps as eager C-ABI launches (default) or one hipGraph replay")
     ap.add_argument("--no-graph", action="store_true", help="same as --launch eager (kept for old scripts)")
-    ap.add_argument("--lead", default="auto", choices=["auto", "replay", "spin", "steps", "none"],
+    ap.add_argument("--lead", default="auto", choices=["auto", "replay", "spin", "steps", "spin-steps", "none"],
                     help="device work enqueued just ahead of the start event: an untimed graph replay, a spin "
-                         "kernel, or (eager) untimed launches of the preceding buffer sets; auto = steps for "
-                         "eager, none for graph")
+                         "kernel, (eager) untimed launches of the preceding buffer sets, or a spin long enough "
+                         "to cover the host's submission of every step followed by those launches; auto = "
+                         "spin-steps for eager, none for graph")
     ap.add_argument("--flush", action="store_true", help="512 MiB Infinity-Cache flush before timing (A/B only)")
     ap.add_argument("--tile-dwords", type=int, default=4)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
@@ -109,6 +114,28 @@ def parse_args(argv=None):
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--dist-backend", default=None, help="nccl (= RCCL, default on GPUs) or gloo (rehearsal)")
     return ap.parse_args(argv)
+
+
+_SPIN_CYCLES_PER_US = [0.0]
+
+
+def _spin_rate_calibrate():
+    """Cycles of torch.cuda._sleep per microsecond on this device (one timed spin)."""
+    import torch
+
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 2_000_000
+    e0.record()
+    torch.cuda._sleep(n)
+    e1.record()
+    torch.cuda.synchronize()
+    _SPIN_CYCLES_PER_US[0] = n / max(e0.elapsed_time(e1) * 1e3, 1.0)
+
+
+def spin_cycles(us: float) -> int:
+    us = min(us, 50_000.0)
+    return int(us * (_SPIN_CYCLES_PER_US[0] or 100.0))
 
 
 # ---------------------------------------------------------------------------
@@ -233,7 +260,7 @@ def find_traffic(m, n, dtype):
 def main():
     args = parse_args()
     if args.lead == "auto":
-        args.lead = "none" if args.launch == "graph" and not args.no_graph else "steps"
+        args.lead = "none" if args.launch == "graph" and not args.no_graph else "spin-steps"
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
@@ -428,6 +455,8 @@ def main():
         del scratch
 
     # ---- timed region --------------------------------------------------------------------
+    if not cpu and args.lead == "spin-steps":
+        _spin_rate_calibrate()
     if world > 1:
         dist.barrier()
     sync()
@@ -447,6 +476,14 @@ def main():
             graph.replay()
         elif args.lead == "spin":
             torch.cuda._sleep(100_000)  # device spin: hides only the host's submission
+        elif graph is None and args.lead == "spin-steps":
+            # a device spin that outlasts the host's submission of every launch below
+            # (a profiler's per-dispatch interception makes submission ~10 us per launch,
+            # slower than the kernels: without the spin the timed launches would trickle
+            # in one by one), then the untimed launches of the preceding sets
+            torch.cuda._sleep(spin_cycles(30.0 * (args.steps + lead_n) + 200.0))
+            for j in range(lead_n):
+                fast[(j - lead_n) % P]()
         elif graph is None and args.lead == "steps":
             # untimed launches of the sets just before the timed ones (steps -L..-1):
             # the queue holds real work when the start event fires, as in a steady
