@@ -66,6 +66,7 @@ GEMM_K128 = 1
 GEMM_STREAM = 2
 GEMM_PERSIST = 3
 GEMM_XS = 4
+GEMM_XR = 5
 
 
 GEMM_GROUP_MAX = 8

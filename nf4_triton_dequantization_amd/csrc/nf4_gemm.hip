@@ -44,6 +44,11 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 #ifndef NF4_XS_DEBUG
 #define NF4_XS_DEBUG 0
 #endif
+// Diagnostic builds of the register-resident kernel (tools/Makefile xrdbg): 1 = no
+// per-strip LDS reduction (no barrier), 2 = no scale gathers, 3 = no dequant / MFMA.
+#ifndef NF4_XR_DEBUG
+#define NF4_XR_DEBUG 0
+#endif
 
 
 // The last arriver's split-K sum for one column group of KCOLS columns: slab
@@ -135,6 +140,7 @@ struct GemmArgs {
     uint32_t chunks_per_split;
     uint32_t chunks;        // K / 128
     uint32_t bpr, groups;   // K / 64, ceil(bpr / 4)
+    uint32_t per_wg;        // register-resident kernel: strips per workgroup
 };
 
 // One 128-deep K chunk of one lane: for each of the wave's NT 16-column strips,
@@ -523,6 +529,237 @@ __global__ __launch_bounds__(64 * WV, 4) void nf4_gemm_xs_kernel(const GemmArgs 
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
     splitk_reduce<DT, 16u>(rs, A.ksplit, A.M, A.ncols, Mt.col_begin + strip * 16u, Mt.y, Mt.N, strip * 16u, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Register-resident activation kernel (NF4DQ_GEMM_XR; K % 128 == 0, any M <= 32).
+// The kernels above re-read x for every column strip they take (from L2 or from
+// an LDS slice staged per workgroup), and cover K with many small slices, so
+// every launch pays a per-workgroup prologue and a wide split-K hand-off.  Here
+// the K split is over the WAVES of one workgroup instead:
+//  * wave w of K slice ks owns KPW 128-deep chunks, (ks * WV + w) * KPW ..; it
+//    loads its x fragments for them ONCE, into registers (MT x 4 x KPW 16-byte
+//    loads per lane), and keeps them for the whole launch;
+//  * the workgroup walks its T column strips (16 columns each, numbered over all
+//    the weights of the launch): per strip a wave needs KPW 16-byte weight loads
+//    per lane plus its scale gathers (reference wrap), held in a D-deep register
+//    ring refilled as each strip is consumed;
+//  * the WV partial 16-column tiles of a strip meet in LDS (double-buffered, one
+//    barrier per strip); one wave per 16-row tile sums them in wave order and
+//    keeps the fp32 result in LDS until the loop ends (no global store among the
+//    ring's loads, so no wait drains the ring);
+//  * WV * KPW * 128 = K needs no split across workgroups (M <= 16, K = 4096:
+//    16 waves x 2 chunks); otherwise ksplit = ceil(K / 128 / (WV * KPW)) slices
+//    meet in the fp32 slab with one ticket per strip, summed in slice order.
+// Same k permutation, dequant and MFMA step as the 128-deep kernel (chunk_mma),
+// so the weights entering the MFMAs are exactly nf4_dequant_ref's.
+// KPW = 1: one 128-deep chunk per wave (lane: 16 B of its row); KPW = 2: one
+// 256-deep chunk (lane: 32 contiguous bytes = one 64-block, so a wave's loads
+// cover whole 128-byte lines of its 16 rows, and one scale per lane).
+template <int KPW>
+struct XSlot {
+    u32x4 w[KPW];
+    uint8_t qa;  // kept 8-bit: a widening right after the load would wait for it (a drained ring)
+    float qb;
+};
+
+// The weight owning a strip: straight-line selects over the group (no loop in
+// the strip loop -- a loop there costs the ring its counted waits)
+__device__ __forceinline__ uint32_t xr_mat_of(const GemmArgs& A, uint32_t strip) {
+    uint32_t mi = 0;
+#pragma unroll
+    for (int i = 1; i < kK128GroupMax; ++i) mi = (uint32_t)i < A.nmat && strip >= A.mat[i].cg_begin ? (uint32_t)i : mi;
+    return mi;
+}
+
+// Lane-constant parts of a strip's offsets (computed once): every per-strip term
+// is then a scalar plus this -- no per-strip vector multiply-add, whose 64-bit
+// form reads an unrelated (possibly still loading) register half and turns the
+// ring's counted waits into drains.
+struct XLane {
+    uint32_t w;   // the lane's bytes within a 16-row chunk: nl K/2 + 16 kh (KPW 1) / 32 kh (KPW 2)
+    uint32_t b1;  // the lane's 64-block within the strip's rows: nl bpr + kh/2 (KPW 1) / kh (KPW 2)
+    uint32_t b2;  // nl * groups
+};
+
+template <int KPW>
+__device__ __forceinline__ void xslot_issue(const GemmArgs& A, uint32_t strip, bool valid, uint32_t cw,
+                                            const XLane& ln, XSlot<KPW>& s) {
+    const K128Mat& Mt = A.mat[xr_mat_of(A, strip)];
+    const uint32_t r0 = (strip - Mt.cg_begin) * 16u;  // first row of the strip (uniform)
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a1, 0, Mt.nb.d, kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a2, 0, Mt.n2.d * 4u, kRsrcFlags);
+    // invalid (past the strips or past K): offsets beyond every range -- zeros, no
+    // traffic, and still one counted load each (a straight-line ring)
+    const uint32_t oob = valid && cw + (uint32_t)(KPW - 1) < A.chunks ? 0u : kOob;
+    // the lane's block: 2 cw + kh/2 (KPW 1) / 4 (cw/2) + kh = 2 cw + kh (KPW 2); its
+    // nested group (block / 4) is cw / 2 either way (uniform)
+    const uint32_t w0 = r0 * (A.K >> 1) + cw * 64u + ln.w;
+#pragma unroll
+    for (int q = 0; q < KPW; ++q) s.w[q] = __builtin_amdgcn_raw_buffer_load_b128(rw, (w0 + 16u * q) | oob, 0, 0);
+#if NF4_XR_DEBUG == 2
+    s.qa = (uint8_t)(fmodu(r0 * A.bpr + 2u * cw + ln.b1, Mt.nb) | 1u);
+    s.qb = __uint_as_float(0x3c000000u | (fmodu(r0 * A.groups + (cw >> 1) + ln.b2, Mt.n2) & 0xFFu));
+    (void)ra1;
+    (void)ra2;
+#else
+    s.qa = __builtin_amdgcn_raw_buffer_load_b8(ra1, fmodu(r0 * A.bpr + 2u * cw + ln.b1, Mt.nb) | oob, 0, 0);  // (:173-177)
+    s.qb = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+        ra2, (fmodu(r0 * A.groups + (cw >> 1) + ln.b2, Mt.n2) * 4u) | oob, 0, 0));  // (:40-41, :183-186)
+#endif
+}
+
+template <int DT, int MT, int WV, int KPW, int D>
+__global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) {
+    extern __shared__ __attribute__((aligned(16))) f32x4 xr_smem[];  // all LDS dynamic (host: xr_lds_bytes)
+    f32x4* red = xr_smem;                                    // [2][WV][MT][64] partial tiles
+    float* lut = reinterpret_cast<float*>(xr_smem + 2 * WV * MT * 64);  // 16 codes
+    uint32_t* last_flags = reinterpret_cast<uint32_t*>(lut + 16);        // [64] split-K tickets drawn last
+    float* held = reinterpret_cast<float*>(last_flags + 64);            // [T][16 MT][16] fp32 results
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t nl = lane & 15u, kh = lane >> 4;
+    const uint32_t S = A.ksplit, T = A.per_wg;
+    const uint32_t ks = blockIdx.x % S;                      // K slice
+    const uint32_t s0 = (blockIdx.x / S) * T;                // first strip (launch-wide)
+    const uint32_t s1 = s0 + T < A.col_groups ? s0 + T : A.col_groups;
+    const uint32_t nst = s1 > s0 ? s1 - s0 : 0u;
+    const uint32_t cw = (ks * (uint32_t)WV + wave) * (uint32_t)KPW;  // the wave's first chunk
+    const XLane ln{nl * (A.K >> 1) + (KPW == 2 ? 32u : 16u) * kh, nl * A.bpr + (KPW == 2 ? kh : kh >> 1),
+                   nl * A.groups};
+
+    // 1. the wave's x fragments (rows >= M and chunks past K read as zeros),
+    //    then the ring's first D strips, then the code table
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
+    u32x4 xf[KPW][MT][4];
+#pragma unroll
+    for (int q = 0; q < KPW; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            // k of fragment (q, s): cw 128 + 32 KPW kh + 32 q + 8 s -- the weight dword's k (same permutation)
+            const uint32_t r = 16u * mt + nl;
+            const uint32_t xoff = r < A.M && cw + (uint32_t)(KPW - 1) < A.chunks
+                                      ? (r * A.K + cw * kChunkK + 32u * KPW * kh + 32u * q) * 2u : kOob;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) xf[q][mt][s] = __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + 16u * s, 0, 0);
+        }
+    __builtin_amdgcn_sched_barrier(0);  // issue order = wait order: x, then the ring slot by slot
+    XSlot<KPW> ring[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        xslot_issue<KPW>(A, s0 + (uint32_t)d, (uint32_t)d < nst, cw, ln, ring[d]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    write_lut(lut);
+    __syncthreads();
+
+    // 2. the strips: dequant + MFMA of the wave's chunks, partial tile to LDS,
+    //    one barrier, the tile's reducer wave sums the WV partials in wave order
+    // Every unrolled step issues its refill, past the last strip too (out of range:
+    // no traffic): with a `break` the loop latch would also be reached right after
+    // step 0's refill, and the waits at the loop head would drain the ring.
+    for (uint32_t t0 = 0; t0 < nst; t0 += (uint32_t)D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const uint32_t t = t0 + (uint32_t)d;
+            const bool live = t < nst;  // uniform
+            f32x4 acc[MT][1];
+            if (live) {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) acc[mt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int q = 0; q < KPW; ++q) {
+                    Chunk<MT, 1> ch;
+                    ch.w[0] = ring[d].w[q];
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int s = 0; s < 4; ++s) ch.x[mt][s] = xf[q][mt][s];
+                    const float scs[1] = {((float)ring[d].qa / 127.0f) * ring[d].qb};  // IEEE division (:45)
+#if NF4_XR_DEBUG == 3
+                    acc[0][0][q & 3] += __uint_as_float((ch.w[0][0] ^ ch.w[0][1] ^ ch.w[0][2] ^ ch.w[0][3]) & 0x3fffffffu) * scs[0];
+#else
+                    chunk_mma<DT, MT, 1>(ch, lut, scs, acc);
+#endif
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            xslot_issue<KPW>(A, s0 + t + (uint32_t)D, t + (uint32_t)D < nst, cw, ln, ring[d]);
+            __builtin_amdgcn_sched_barrier(0);
+#if NF4_XR_DEBUG == 1
+            if (live && wave == 0) {
+                float* h = held + t * (16u * MT * 16u) + 4u * kh * 16u + nl;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) h[16u * r] = acc[0][0][r];
+            }
+            if (false) {
+#else
+            if (live) {
+#endif
+                f32x4* rb = red + (t & 1u) * (WV * MT * 64);
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) rb[(wave * MT + mt) * 64 + lane] = acc[mt][0];
+                __syncthreads();
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    if (wave == (t * MT + (uint32_t)mt) % (uint32_t)WV) {  // uniform
+                        f32x4 sum = rb[mt * 64 + lane];
+#pragma unroll
+                        for (int w = 1; w < WV; ++w) sum += rb[(w * MT + mt) * 64 + lane];
+                        // sum[r] = Y[16 mt + 4 kh + r][strip col nl]
+                        float* h = held + t * (16u * MT * 16u) + (16u * mt + 4u * kh) * 16u + nl;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) h[16u * r] = sum[r];
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // 3. the results: straight to y (one slice), or to the slab + tickets
+    const uint32_t rows = A.M;
+    if (S == 1) {
+        // 16-bit pairs, a row's 16 columns = 8 consecutive dwords
+        for (uint32_t e = tid; e < nst * rows * 8u; e += 64u * WV) {
+            const uint32_t t = e / (rows * 8u), rem = e - t * rows * 8u, m = rem >> 3, p = rem & 7u;
+            const uint32_t strip = s0 + t;
+            const K128Mat& Mt = A.mat[xr_mat_of(A, strip)];
+            const float* h = held + t * (16u * MT * 16u) + m * 16u + 2u * p;
+            uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(Mt.y) + m * Mt.N +
+                                                        (strip - Mt.cg_begin) * 16u + 2u * p);
+            *dst = pack2<DT>(h[0], h[1]);
+        }
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)A.slab, 0, A.ksplit * A.M * A.ncols * 4u, kRsrcFlags);
+    // slab [ks][M][ncols] fp32 (strip s at columns 16 s), write-through, drained
+    for (uint32_t e = tid; e < nst * rows * 4u; e += 64u * WV) {
+        const uint32_t t = e / (rows * 4u), rem = e - t * rows * 4u, m = rem >> 2, p = rem & 3u;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(held + t * (16u * MT * 16u) + m * 16u + 4u * p);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs,
+                                               ((ks * A.M + m) * A.ncols + (s0 + t) * 16u + 4u * p) * 4u, 0, kAuxSc1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's slab stores are out
+    __syncthreads();
+    if (tid < nst) {  // one ticket per strip; nst <= 64 (host-checked)
+        const uint32_t strip = s0 + tid;
+        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[strip], 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t last = ticket == S - 1u;
+        if (last) __hip_atomic_store(&A.counters[strip], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_flags[tid] = last;
+    }
+    __syncthreads();
+    for (uint32_t t = wave; t < nst; t += (uint32_t)WV) {
+        if (!last_flags[t]) continue;  // uniform
+        const uint32_t strip = s0 + t;
+        const K128Mat& Mt = A.mat[xr_mat_of(A, strip)];
+        const uint32_t lc = (strip - Mt.cg_begin) * 16u;
+        splitk_reduce<DT, 16u>(rs, S, A.M, A.ncols, strip * 16u, Mt.y, Mt.N, lc, lane);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1294,6 +1531,15 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
         if (c.ksplit < 1 || c.ksplit > K / kSChunkK) return false;
         return stream_fits(M, K, c);
     }
+    if (c.kernel == NF4DQ_GEMM_XR) {
+        if (c.waves != 8 && c.waves != 16) return false;
+        if (c.depth != 2 && c.depth != 4) return false;
+        if (c.strips != 1 && c.strips != 2) return false;  // 128-deep chunks per wave
+        if (M > 16 && c.strips == 2 && c.depth == 4) return false;  // x + ring beyond the registers (spills)
+        if (c.strips == 2 && K % 256) return false;                 // 256-deep chunks
+        const int64_t chunks = K / kChunkK, per = (int64_t)c.waves * c.strips;
+        return c.ksplit == (chunks + per - 1) / per && c.ksplit <= 1024;
+    }
     if (c.kernel == NF4DQ_GEMM_XS) {
         if (c.waves != 4 && c.waves != 8) return false;
         if (c.depth != 2 && c.depth != 4 && c.depth != 8) return false;
@@ -1621,6 +1867,99 @@ static int launch_xs(const HostMat* mats, int count, const void* x, int64_t M, i
     return hip_rc2(hipGetLastError());
 }
 
+// Register-resident kernel: grid = ksplit x (strip groups of T strips); T from
+// the CUs the launch can hold at once (one 16-wave workgroup per CU), at most 64
+// (ticket flags) and within LDS.
+static uint32_t xr_lds_bytes(int64_t M, int waves, uint32_t T) {
+    const uint32_t mt = M > 16 ? 2u : 1u;
+    return 2u * (uint32_t)waves * mt * 1024u + 64u + 256u + T * mt * 1024u;  // partials, codes, flags, held
+}
+
+static uint32_t xr_per_wg(int64_t M, int64_t strips, const nf4_gemm_cfg& c) {
+    const uint32_t wg_per_cu = c.waves == 16 ? 1u : 2u;
+    uint32_t P = (uint32_t)device_cus() * wg_per_cu / (uint32_t)c.ksplit;  // workgroups per K slice
+    if (P < 1) P = 1;
+    uint32_t T = (uint32_t)((strips + P - 1) / P);
+    while (T > 1 && (T > 64 || xr_lds_bytes(M, c.waves, T) > kLdsPerCu)) T = (T + 1) / 2;
+    return T < 1 ? 1u : T;
+}
+
+static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
+                     const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st) {
+    const uint32_t ks = (uint32_t)cfg.ksplit;
+    GemmArgs A{};
+    A.nmat = (uint32_t)count;
+    A.x = x;
+    A.counters = reinterpret_cast<uint32_t*>(workspace);
+    A.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    A.M = (uint32_t)M;
+    A.K = (uint32_t)K;
+    A.ksplit = ks;
+    A.chunks = (uint32_t)(K / kChunkK);
+    A.chunks_per_split = (uint32_t)(cfg.waves * cfg.strips);
+    A.bpr = (uint32_t)(K / 64);
+    A.groups = (A.bpr + 3) / 4;
+    uint32_t strips = 0;
+    for (int i = 0; i < count; ++i) {
+        const HostMat& h = mats[i];
+        K128Mat& m = A.mat[i];
+        m.packed = h.packed;
+        m.a1 = h.a1;
+        m.a2 = h.a2;
+        m.y = h.y;
+        m.N = (uint32_t)h.N;
+        m.cg_begin = strips;        // first 16-column strip of the weight in the launch
+        m.col_begin = strips * 16u;
+        m.nb = make_fastdiv((uint32_t)(h.nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : h.nb));
+        m.n2 = make_fastdiv((uint32_t)(h.n2 > (int64_t(1) << 29) ? (int64_t(1) << 29) : h.n2));
+        strips += (uint32_t)(h.N / 16);
+    }
+    A.col_groups = strips;
+    A.ncols = strips * 16u;
+    A.per_wg = xr_per_wg(M, strips, cfg);
+    const uint32_t groups = (strips + A.per_wg - 1) / A.per_wg;
+    const dim3 grid(groups * ks), block(64 * cfg.waves);
+    const uint32_t lds = xr_lds_bytes(M, cfg.waves, A.per_wg);
+#define NF4_R1(DT_, MT_, W_, KPW_, D_)                                                                               \
+    do {                                                                                                             \
+        static bool attr_ = false; /* dynamic LDS above 64 KiB needs the opt-in */                                   \
+        if (!attr_) {                                                                                                \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_xr_kernel<DT_, MT_, W_, KPW_, D_>),    \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);                   \
+            attr_ = true;                                                                                            \
+        }                                                                                                            \
+        hipLaunchKernelGGL((nf4_gemm_xr_kernel<DT_, MT_, W_, KPW_, D_>), grid, block, lds, st, A);                   \
+    } while (0)
+#define NF4_RD(DT_, MT_, W_, KPW_)                         \
+    do {                                                   \
+        if (cfg.depth == 4) NF4_R1(DT_, MT_, W_, KPW_, 4); \
+        else NF4_R1(DT_, MT_, W_, KPW_, 2);                \
+    } while (0)
+#define NF4_RK(DT_, MT_, W_)                          \
+    do {                                              \
+        if (cfg.strips == 2) NF4_RD(DT_, MT_, W_, 2); \
+        else NF4_RD(DT_, MT_, W_, 1);                 \
+    } while (0)
+#define NF4_RW(DT_, MT_)                          \
+    do {                                          \
+        if (cfg.waves == 16) NF4_RK(DT_, MT_, 16); \
+        else NF4_RK(DT_, MT_, 8);                 \
+    } while (0)
+#define NF4_RM(DT_)                 \
+    do {                            \
+        if (M > 16) NF4_RW(DT_, 2); \
+        else NF4_RW(DT_, 1);        \
+    } while (0)
+    if (dtype == NF4DQ_BF16) NF4_RM(NF4DQ_BF16);
+    else NF4_RM(NF4DQ_F16);
+#undef NF4_RM
+#undef NF4_RW
+#undef NF4_RK
+#undef NF4_RD
+#undef NF4_R1
+    return hip_rc2(hipGetLastError());
+}
+
 static int launch_k128(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
                        const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st) {
     const uint32_t ks = (uint32_t)cfg.ksplit;
@@ -1737,6 +2076,7 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     }
     const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
     if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(&h, 1, x, M, K, dtype, cfg, workspace, st);
+    if (cfg.kernel == NF4DQ_GEMM_XR) return launch_xr(&h, 1, x, M, K, dtype, cfg, workspace, st);
     return launch_k128(&h, 1, x, M, K, dtype, cfg, workspace, st);
 }
 
@@ -1767,7 +2107,9 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
     for (int i = 0; i < count; ++i) {
         // an empty weight cannot own strip groups (the 128-deep kernel numbers
         // column groups per weight: an empty one simply owns none)
-        if (mats[i].N == 0 && cfg.kernel != NF4DQ_GEMM_K128 && cfg.kernel != NF4DQ_GEMM_XS) return NF4DQ_ERR_SHAPE;
+        if (mats[i].N == 0 && cfg.kernel != NF4DQ_GEMM_K128 && cfg.kernel != NF4DQ_GEMM_XS &&
+            cfg.kernel != NF4DQ_GEMM_XR)
+            return NF4DQ_ERR_SHAPE;
         if (mats[i].N == 0) continue;
         if (!valid_gemm_cfg(cfg, M, mats[i].N, K)) return NF4DQ_ERR_ARG;
         if (mats[i].packed_len >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
@@ -1781,6 +2123,7 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
                        mats[i].n2, mats[i].y, mats[i].N};
     if (cfg.kernel == NF4DQ_GEMM_K128) return launch_k128(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(h, count, x, M, K, dtype, cfg, workspace, st);
+    if (cfg.kernel == NF4DQ_GEMM_XR) return launch_xr(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
         const int rc = launch_persist(h, count, x, M, K, dtype, cfg, workspace, st);
         if ((rc != NF4DQ_ERR_ARG && rc != NF4DQ_ERR_TOO_LARGE) || cfgp) return rc;

@@ -528,3 +528,92 @@ def test_shared_activation_kernel_grouped(coracle, gpu, wrap):
         for y, W in zip(ys, Ws):
             _check(y, xb, W, "bf16")
         assert int(ws[:65536].view(torch.int32).abs().sum()) == 0  # tickets back at 0
+
+
+def _xr_cfg(_lib, K, waves, depth, kpw):
+    return _lib.GemmCfg(_lib.GEMM_XR, waves, depth, -(-(K // 128) // (waves * kpw)), kpw)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,N,K", [(32, 1024, 4096), (17, 192, 1280), (24, 448, 384), (1, 64, 128), (9, 320, 2304),
+                                   (32, 64, 11008), (16, 4160, 4096), (3, 2048, 4096)])
+def test_register_resident_kernel_vs_oracle(coracle, gpu, dt, M, N, K):
+    """NF4DQ_GEMM_XR, every (waves, depth, chunk depth) it accepts: one K slice
+    (no slab: K = 4096 with 16 x 256-deep chunks) and several (the last one
+    partial when K/128 is not a multiple), rows >= M padded, strips per workgroup
+    from 1 up to the ring depth and beyond (partial last ring round)."""
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    packed, a1, a2 = O.make_inputs(N, K, seed=N + 5 * K + M, a2_kind="normal")
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16)
+    t = (torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu))
+    xt, xb = _x_bits(M, K, dt, seed=M * 11 + 5)
+    x = xt.to(gpu)
+    code = _lib.BF16 if dt == "bf16" else _lib.F16
+    y = torch.empty((M, N), dtype=x.dtype, device=gpu)
+    ran = 0
+    for waves in (8, 16):
+        for depth in (2, 4):
+            for kpw in (1, 2):
+                cfg = _xr_cfg(_lib, K, waves, depth, kpw)
+                if (M > 16 and kpw == 2 and depth == 4) or (kpw == 2 and K % 256):
+                    assert _gemm_cfg_call(L, _lib, x, t, y, code, N, K, cfg) == _lib.ERR_ARG
+                    continue
+                for _ in range(2):  # twice: the tickets the first call left at 0 are reused
+                    y.fill_(float("nan"))
+                    rc = _gemm_cfg_call(L, _lib, x, t, y, code, N, K, cfg)
+                    assert rc == 0, (waves, depth, kpw, rc)
+                    _check(y, xb, W, dt)
+                ran += 1
+    assert ran == (4 if K % 256 else 6 if M > 16 else 8)
+    bad = _lib.GemmCfg(_lib.GEMM_XR, 16, 2, -(-(K // 128) // 16) + 1, 1)  # ksplit must be ceil(chunks / 16)
+    assert _gemm_cfg_call(L, _lib, x, t, y, code, N, K, bad) == _lib.ERR_ARG
+
+
+@pytest.mark.parametrize("wrap", [False, True])
+@pytest.mark.parametrize("M", [8, 32])
+def test_register_resident_kernel_grouped(coracle, gpu, wrap, M):
+    """One grouped launch of the register-resident kernel (q/k/v-like widths, an
+    empty weight in the middle); `wrap` adds a weight whose absmax / nested
+    absmax wrap inside rows (per-lane gathers with the reference's modular
+    indices)."""
+    import ctypes
+
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    K = 2048
+    Ns = (1024, 0, 256, 320) + ((128,) if wrap else ())
+    mats = (_lib.GemmMat * len(Ns))()
+    ys, keep, Ws = [], [], []
+    for i, N in enumerate(Ns):
+        if wrap and i == 4:
+            packed, a1, a2 = O.golden_case_inputs(N, K, 5, {"nb": 37, "n2": 5})[:3]
+        elif N == 0:
+            packed, a1, a2 = (np.zeros(16, np.uint8), np.ones(4, np.uint8), np.ones(1, np.float32))
+        else:
+            packed, a1, a2 = O.make_inputs(N, K, seed=7 * N + i, a2_kind="normal")
+        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16) if N else None)
+        tt = [torch.from_numpy(v).to(gpu) for v in (packed, a1, a2)]
+        keep.append(tt)
+        y = torch.full((M, max(N, 1)), float("nan"), dtype=torch.bfloat16, device=gpu)
+        ys.append(y)
+        mats[i] = _lib.GemmMat(tt[0].data_ptr(), N * K // 2, tt[1].data_ptr(), tt[1].numel(), tt[2].data_ptr(),
+                               tt[2].numel(), y.data_ptr(), N)
+    xt, xb = _x_bits(M, K, "bf16", seed=67 + M)
+    x = xt.to(gpu)
+    for waves, depth, kpw in ((16, 4, 1), (16, 2, 2), (8, 2, 1), (8, 4, 1)):
+        c = _xr_cfg(_lib, K, waves, depth, kpw)
+        wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, mats, len(Ns), ctypes.byref(c))
+        ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=gpu)
+        for y in ys:
+            y.fill_(float("nan"))
+        rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, mats, len(Ns), _lib.BF16, ws.data_ptr(), wsz,
+                                    ctypes.byref(c), torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+        for y, W in zip(ys, Ws):
+            if W is not None:
+                _check(y, xb, W, "bf16")
+        assert int(ws[:65536].view(torch.int32).abs().sum()) == 0  # tickets back at 0

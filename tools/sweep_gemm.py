@@ -52,8 +52,9 @@ def main():
     ap.add_argument("--ms", default="1,16,32")
     ap.add_argument("--budget-mb", type=int, default=768, help="packed weight bytes per shape")
     ap.add_argument("--shapes", default="", help="N,K;N,K;... (default: the Llama-3-8B list)")
-    ap.add_argument("--kernels", default="1,2,3,4",
-                    help="kernel ids to sweep (1 K128, 2 stream, 3 persist, 4 shared-activation)")
+    ap.add_argument("--kernels", default="1,2,3,4,5",
+                    help="kernel ids to sweep (1 K128, 2 stream, 3 persist, 4 shared-activation, "
+                         "5 register-resident)")
     args = ap.parse_args()
     shapes = [tuple(int(v) for v in s.split(",")) for s in args.shapes.split(";")] if args.shapes else SHAPES
     kern = {int(v) for v in args.kernels.split(",")}
@@ -91,6 +92,10 @@ def main():
             for waves in (4, 8):
                 for kc in (2, 4, 8):  # shared-activation kernel: chunks per K slice; ksplit follows
                     cfgs.append(_lib.GemmCfg(_lib.GEMM_XS, waves, kc, -(-(k // 128) // kc), 1))
+            for waves in (8, 16):
+                for depth in (2, 4):
+                    for kpw in (1, 2):  # register-resident kernel: chunks per wave; ksplit follows
+                        cfgs.append(_lib.GemmCfg(_lib.GEMM_XR, waves, depth, -(-(k // 128) // (waves * kpw)), kpw))
             cfgs = [c for c in cfgs if c.kernel in kern]
             for cfg in cfgs:
                 wsz = L.nf4_gemm_workspace_bytes_cfg(M, n, k, ctypes.byref(cfg))
