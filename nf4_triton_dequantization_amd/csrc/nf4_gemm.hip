@@ -1467,6 +1467,13 @@ static nf4_gemm_cfg nonpersist_cfg(int64_t M, int64_t N, int64_t K) {
         return k128_cfg(M, N, K, 8, 2, 1, 1);
     }
     if (K >= 8192) return k128_cfg(M, N, K, 8, 1, 4, 4);
+    if (N >= 16384 && K % kSChunkK == 0) {
+        // the widest launches (grouped gate/up): the register-resident kernel, 16 waves x
+        // 256-deep chunks (no K split at K = 4096): 35.3 vs 37.9 us (shared-activation)
+        // at M = 32 on 28672 x 4096 (profiles/r02/sweep_gemm_xr.jsonl)
+        const nf4_gemm_cfg c{NF4DQ_GEMM_XR, 16, 2, (int)((K / kChunkK + 31) / 32), 2};
+        if (valid_gemm_cfg(c, M, N, K)) return c;
+    }
     if (N >= 6144) {
         // wide launches (gate/up, grouped q/k/v): the shared-activation kernel,
         // 10-13 % faster than the 128-deep one at M = 24 / 32 (profiles/r02/sweep_gemm_xs.jsonl)
