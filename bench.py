@@ -269,6 +269,11 @@ def main():
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; they must agree")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # stdout carries exactly one line, the result: anything the runtime libraries
+    # print there (gloo's connection notes, RCCL / HIP warnings) goes to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -580,7 +585,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not cpu:
         res["cpu_baseline"] = cpu_baseline(mats, args.cpu_seconds, code)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=result_out, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
