@@ -21,7 +21,7 @@ WORLD_SIZE must equal N.
 Timed region (``value``): K steps as K eager launches of the product C-ABI entry
 (``nf4_dequant_ref``, arguments prepared up front), bracketed by barrier +
 synchronize on both sides, HIP events on the launch stream around them.  Ahead of
-the start event sit L = 8 untimed launches of the preceding buffer sets, so the
+the start event sit L = 16 untimed launches of the preceding buffer sets, so the
 queue holds real work when timing starts, as in a steady stream of weights, and
 ahead of those a device spin that outlasts the host's submission of all L + K
 launches (``--lead spin-steps``): the K kernels then run back to back even when
@@ -104,6 +104,7 @@ def parse_args(argv=None):
                          "kernel, (eager) untimed launches of the preceding buffer sets, or a spin long enough "
                          "to cover the host's submission of every step followed by those launches; auto = "
                          "spin-steps for eager, none for graph")
+    ap.add_argument("--lead-n", type=int, default=16, help="untimed launches just ahead of the start event (<= sets)")
     ap.add_argument("--flush", action="store_true", help="512 MiB Infinity-Cache flush before timing (A/B only)")
     ap.add_argument("--tile-dwords", type=int, default=4)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
@@ -410,7 +411,7 @@ def main():
                 if rc:
                     raise RuntimeError(f"nf4 dequant launch: {_lib.strerror(rc)}")
             fast.append(call)
-    lead_n = min(8, P)
+    lead_n = min(args.lead_n, P)
 
     # correctness sanity of set 0 against the oracle on the first 64 rows of each
     # matrix (the checker; tests/ do the full job)
