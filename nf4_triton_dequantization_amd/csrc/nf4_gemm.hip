@@ -45,7 +45,8 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 #define NF4_XS_DEBUG 0
 #endif
 // Diagnostic builds of the register-resident kernel (tools/Makefile xrdbg): 1 = no
-// per-strip LDS reduction (no barrier), 2 = no scale gathers, 3 = no dequant / MFMA.
+// per-strip LDS reduction (no barrier), 2 = no scale gathers, 3 = no dequant / MFMA,
+// 4 = 256-deep chunks through the 16-entry code table instead of the pair table.
 #ifndef NF4_XR_DEBUG
 #define NF4_XR_DEBUG 0
 #endif
@@ -610,11 +611,73 @@ __device__ __forceinline__ void xslot_issue(const GemmArgs& A, uint32_t strip, b
 #endif
 }
 
+// Dequant + MFMA of one 256-deep chunk with the activations in registers (KPW = 2):
+// the streaming kernel's pair-table lookups (sslot_mma: one conflict-free
+// ds_read_b64 per packed byte = two weights, issued LA steps ahead), the fp32
+// products with the block scale, one RNE pack per pair; x fragment (q, s) of step
+// st = 4 q + s carries the same k as weight dword st (same permutation).
+template <int DT, int MT>
+__device__ __forceinline__ void xr_pair_mma(const u32x4& w0, const u32x4& w1, float sc, const f32x2* ptab,
+                                            uint32_t slot8, const u32x4 (&xf)[2][MT][4], f32x4 (&acc)[MT]) {
+    const f32x2 sc2 = {sc, opaque(sc)};
+    const char* pt = reinterpret_cast<const char*>(ptab);
+    // MT = 2 holds 64 VGPRs of x: a shorter lookahead, and its two row tiles already
+    // give two independent MFMA chains (no second accumulator set)
+    constexpr int LA = MT == 2 ? 2 : 3;
+    f32x2 v[8][4];
+    f32x4 accb[MT == 2 ? 1 : MT];
+#pragma unroll
+    for (int mt = 0; mt < (MT == 2 ? 1 : MT); ++mt) accb[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto issue = [&](int st) {
+        const uint32_t wd = st < 4 ? w0[st] : w1[st - 4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t addr = __builtin_amdgcn_perm(wd, slot8, 0x0C0C0000u | ((4u + b) << 8));
+            v[st][b] = *reinterpret_cast<const f32x2*>(pt + addr);
+        }
+    };
+#pragma unroll
+    for (int st = 0; st < LA; ++st) issue(st);
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+        if (st + LA < 8) issue(st + LA);
+        // required for correctness, not speed: without it the scheduler interleaves
+        // the next refill's scalar loads (lgkmcnt, completing out of order) with these
+        // counted LDS waits, and every strip after a workgroup's first came out wrong
+        // (tools/xr_probe.py)
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t bw[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const f32x2 p = v[st][b] * sc2;  // fp32 products (:97-98)
+            bw[b] = pack2<DT>(p.x, p.y);     // RNE (:109-110)
+        }
+        const u32x4 bq = {bw[0], bw[1], bw[2], bw[3]};
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            f32x4& c = (MT == 1 && (st & 1)) ? accb[0] : acc[mt];
+            const u32x4 a = xf[st >> 2][mt][st & 3];
+            if constexpr (DT == NF4DQ_BF16) {
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, bq),
+                                                            c, 0, 0, 0);
+            } else {
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, bq),
+                                                           c, 0, 0, 0);
+            }
+        }
+    }
+    if constexpr (MT == 1) acc[0] += accb[0];
+}
+
 template <int DT, int MT, int WV, int KPW, int D>
 __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) {
     extern __shared__ __attribute__((aligned(16))) f32x4 xr_smem[];  // all LDS dynamic (host: xr_lds_bytes)
-    f32x4* red = xr_smem;                                    // [2][WV][MT][64] partial tiles
-    float* lut = reinterpret_cast<float*>(xr_smem + 2 * WV * MT * 64);  // 16 codes
+    // KPW = 2: the pair table (64 KiB) and the q/127 table lead the region
+    constexpr int kPt = KPW == 2 ? (256 * 32 * 8 + 1024) / 16 : 0;  // in f32x4
+    f32x2* ptab = reinterpret_cast<f32x2*>(xr_smem);
+    float* qtab = reinterpret_cast<float*>(xr_smem + (256 * 32 * 8) / 16);
+    f32x4* red = xr_smem + kPt;                              // [2][WV][MT][64] partial tiles
+    float* lut = reinterpret_cast<float*>(red + 2 * WV * MT * 64);      // 16 codes
     uint32_t* last_flags = reinterpret_cast<uint32_t*>(lut + 16);        // [64] split-K tickets drawn last
     float* held = reinterpret_cast<float*>(last_flags + 64);            // [T][16 MT][16] fp32 results
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -652,6 +715,15 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
         __builtin_amdgcn_sched_barrier(0);
     }
     write_lut(lut);
+    if constexpr (KPW == 2) {  // tables while the loads fly (as the streaming kernels)
+        if (tid < 256u) qtab[tid] = (float)tid / 127.0f;  // IEEE division (:45)
+        for (uint32_t u = tid; u < 16u * 32u; u += 64u * WV) {
+            const float clo = nf4_code(u >> 5);
+#pragma unroll
+            for (int hi = 0; hi < 16; ++hi) ptab[(16u * hi + (u >> 5)) * 32u + (u & 31u)] = f32x2{nf4_code(hi), clo};
+        }
+    }
+    const uint32_t slot8 = (lane & 31u) * 8u;
     __syncthreads();
 
     // 2. the strips: dequant + MFMA of the wave's chunks, partial tile to LDS,
@@ -668,8 +740,16 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
             if (live) {
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt) acc[mt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if constexpr (KPW == 2 && NF4_XR_DEBUG != 4) {
+                    f32x4 a2[MT];
 #pragma unroll
-                for (int q = 0; q < KPW; ++q) {
+                    for (int mt = 0; mt < MT; ++mt) a2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    xr_pair_mma<DT, MT>(ring[d].w[0], ring[d].w[1], qtab[ring[d].qa] * ring[d].qb, ptab, slot8, xf, a2);
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) acc[mt][0] = a2[mt];
+                }
+#pragma unroll
+                for (int q = 0; q < (KPW == 2 && NF4_XR_DEBUG != 4 ? 0 : KPW); ++q) {
                     Chunk<MT, 1> ch;
                     ch.w[0] = ring[d].w[q];
 #pragma unroll
@@ -1466,14 +1546,15 @@ static nf4_gemm_cfg nonpersist_cfg(int64_t M, int64_t N, int64_t K) {
         if (N < 4096) return k128_cfg(M, N, K, 4, 2, 4, 1);
         return k128_cfg(M, N, K, 8, 2, 1, 1);
     }
-    if (K >= 8192) return k128_cfg(M, N, K, 8, 1, 4, 4);
-    if (N >= 16384 && K % kSChunkK == 0) {
-        // the widest launches (grouped gate/up): the register-resident kernel, 16 waves x
-        // 256-deep chunks (no K split at K = 4096): 35.3 vs 37.9 us (shared-activation)
-        // at M = 32 on 28672 x 4096 (profiles/r02/sweep_gemm_xr.jsonl)
-        const nf4_gemm_cfg c{NF4DQ_GEMM_XR, 16, 2, (int)((K / kChunkK + 31) / 32), 2};
+    if (K % kSChunkK == 0 && N >= 2048) {
+        // the register-resident kernel with pair-table lookups, 8 waves x 256-deep
+        // chunks: per launch at M = 32 (profiles/r02/sweep_gemm_xr.jsonl) 20.4 vs 21.7 us
+        // on 14336x4096, 11.9 vs 12.3 on 4096^2, 23.5 vs 24.6 on 4096x14336, 13.8 vs 14.2
+        // on grouped q/k/v (6144), 31.4 vs 37.2 on grouped gate/up (28672)
+        const nf4_gemm_cfg c{NF4DQ_GEMM_XR, 8, 2, (int)((K / kChunkK + 15) / 16), 2};
         if (valid_gemm_cfg(c, M, N, K)) return c;
     }
+    if (K >= 8192) return k128_cfg(M, N, K, 8, 1, 4, 4);
     if (N >= 6144) {
         // wide launches (gate/up, grouped q/k/v): the shared-activation kernel,
         // 10-13 % faster than the 128-deep one at M = 24 / 32 (profiles/r02/sweep_gemm_xs.jsonl)
@@ -1877,17 +1958,18 @@ static int launch_xs(const HostMat* mats, int count, const void* x, int64_t M, i
 // Register-resident kernel: grid = ksplit x (strip groups of T strips); T from
 // the CUs the launch can hold at once (one 16-wave workgroup per CU), at most 64
 // (ticket flags) and within LDS.
-static uint32_t xr_lds_bytes(int64_t M, int waves, uint32_t T) {
+static uint32_t xr_lds_bytes(int64_t M, int waves, int kpw, uint32_t T) {
     const uint32_t mt = M > 16 ? 2u : 1u;
-    return 2u * (uint32_t)waves * mt * 1024u + 64u + 256u + T * mt * 1024u;  // partials, codes, flags, held
+    const uint32_t tables = kpw == 2 ? 256u * 32u * 8u + 1024u : 0u;  // pair table + q/127 (256-deep chunks)
+    return tables + 2u * (uint32_t)waves * mt * 1024u + 64u + 256u + T * mt * 1024u;  // partials, codes, flags, held
 }
 
 static uint32_t xr_per_wg(int64_t M, int64_t strips, const nf4_gemm_cfg& c) {
-    const uint32_t wg_per_cu = c.waves == 16 ? 1u : 2u;
+    const uint32_t wg_per_cu = c.waves == 16 || c.strips == 2 ? 1u : 2u;  // the pair table leaves room for one
     uint32_t P = (uint32_t)device_cus() * wg_per_cu / (uint32_t)c.ksplit;  // workgroups per K slice
     if (P < 1) P = 1;
     uint32_t T = (uint32_t)((strips + P - 1) / P);
-    while (T > 1 && (T > 64 || xr_lds_bytes(M, c.waves, T) > kLdsPerCu)) T = (T + 1) / 2;
+    while (T > 1 && (T > 64 || xr_lds_bytes(M, c.waves, c.strips, T) > kLdsPerCu)) T = (T + 1) / 2;
     return T < 1 ? 1u : T;
 }
 
@@ -1926,7 +2008,7 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
     A.per_wg = xr_per_wg(M, strips, cfg);
     const uint32_t groups = (strips + A.per_wg - 1) / A.per_wg;
     const dim3 grid(groups * ks), block(64 * cfg.waves);
-    const uint32_t lds = xr_lds_bytes(M, cfg.waves, A.per_wg);
+    const uint32_t lds = xr_lds_bytes(M, cfg.waves, cfg.strips, A.per_wg);
 #define NF4_R1(DT_, MT_, W_, KPW_, D_)                                                                               \
     do {                                                                                                             \
         static bool attr_ = false; /* dynamic LDS above 64 KiB needs the opt-in */                                   \

@@ -564,7 +564,10 @@ def test_register_resident_kernel_vs_oracle(coracle, gpu, dt, M, N, K):
                     y.fill_(float("nan"))
                     rc = _gemm_cfg_call(L, _lib, x, t, y, code, N, K, cfg)
                     assert rc == 0, (waves, depth, kpw, rc)
-                    _check(y, xb, W, dt)
+                    try:
+                        _check(y, xb, W, dt)
+                    except AssertionError as e:
+                        raise AssertionError(f"cfg waves={waves} depth={depth} kpw={kpw}: {e}") from None
                 ran += 1
     assert ran == (4 if K % 256 else 6 if M > 16 else 8)
     bad = _lib.GemmCfg(_lib.GEMM_XR, 16, 2, -(-(K // 128) // 16) + 1, 1)  # ksplit must be ceil(chunks / 16)
