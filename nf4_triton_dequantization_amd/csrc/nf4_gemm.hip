@@ -1623,7 +1623,8 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
         if (c.waves != 8 && c.waves != 16) return false;
         if (c.depth != 2 && c.depth != 4) return false;
         if (c.strips != 1 && c.strips != 2) return false;  // 128-deep chunks per wave
-        if (M > 16 && c.strips == 2 && c.depth == 4) return false;  // x + ring beyond the registers (spills)
+        // x + a 4-deep ring spill within 16 waves' 128 registers (8 waves: 256)
+        if (M > 16 && c.strips == 2 && c.depth == 4 && c.waves == 16) return false;
         if (c.strips == 2 && K % 256) return false;                 // 256-deep chunks
         const int64_t chunks = K / kChunkK, per = (int64_t)c.waves * c.strips;
         return c.ksplit == (chunks + per - 1) / per && c.ksplit <= 1024;
