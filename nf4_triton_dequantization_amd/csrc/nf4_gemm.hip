@@ -676,8 +676,10 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     constexpr int kPt = KPW == 2 ? (256 * 32 * 8 + 1024) / 16 : 0;  // in f32x4
     f32x2* ptab = reinterpret_cast<f32x2*>(xr_smem);
     float* qtab = reinterpret_cast<float*>(xr_smem + (256 * 32 * 8) / 16);
-    f32x4* red = xr_smem + kPt;                              // [2][WV][MT][64] partial tiles
-    float* lut = reinterpret_cast<float*>(red + 2 * WV * MT * 64);      // 16 codes
+    // partial tiles meet once per R strips (8 waves: two strips per barrier)
+    constexpr int R = WV == 8 && D % 2 == 0 ? 2 : 1;
+    f32x4* red = xr_smem + kPt;                              // [2][R][WV][MT][64] partial tiles
+    float* lut = reinterpret_cast<float*>(red + 2 * R * WV * MT * 64);  // 16 codes
     uint32_t* last_flags = reinterpret_cast<uint32_t*>(lut + 16);        // [64] split-K tickets drawn last
     float* held = reinterpret_cast<float*>(last_flags + 64);            // [T][16 MT][16] fp32 results
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -732,21 +734,17 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     // no traffic): with a `break` the loop latch would also be reached right after
     // step 0's refill, and the waits at the loop head would drain the ring.
     for (uint32_t t0 = 0; t0 < nst; t0 += (uint32_t)D) {
+        f32x4 accs[R][MT];  // the partials of the current reduction group (R strips)
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             const uint32_t t = t0 + (uint32_t)d;
             const bool live = t < nst;  // uniform
-            f32x4 acc[MT][1];
+            f32x4 (&acc)[MT] = accs[d % R];
             if (live) {
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) acc[mt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if constexpr (KPW == 2 && NF4_XR_DEBUG != 4) {
-                    f32x4 a2[MT];
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt) a2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    xr_pair_mma<DT, MT>(ring[d].w[0], ring[d].w[1], qtab[ring[d].qa] * ring[d].qb, ptab, slot8, xf, a2);
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt) acc[mt][0] = a2[mt];
+                    xr_pair_mma<DT, MT>(ring[d].w[0], ring[d].w[1], qtab[ring[d].qa] * ring[d].qb, ptab, slot8, xf, acc);
                 }
 #pragma unroll
                 for (int q = 0; q < (KPW == 2 && NF4_XR_DEBUG != 4 ? 0 : KPW); ++q) {
@@ -757,40 +755,63 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
 #pragma unroll
                         for (int s = 0; s < 4; ++s) ch.x[mt][s] = xf[q][mt][s];
                     const float scs[1] = {((float)ring[d].qa / 127.0f) * ring[d].qb};  // IEEE division (:45)
+                    f32x4 a1[MT][1];
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) a1[mt][0] = acc[mt];
 #if NF4_XR_DEBUG == 3
-                    acc[0][0][q & 3] += __uint_as_float((ch.w[0][0] ^ ch.w[0][1] ^ ch.w[0][2] ^ ch.w[0][3]) & 0x3fffffffu) * scs[0];
+                    a1[0][0][q & 3] += __uint_as_float((ch.w[0][0] ^ ch.w[0][1] ^ ch.w[0][2] ^ ch.w[0][3]) & 0x3fffffffu) * scs[0];
 #else
-                    chunk_mma<DT, MT, 1>(ch, lut, scs, acc);
+                    chunk_mma<DT, MT, 1>(ch, lut, scs, a1);
 #endif
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) acc[mt] = a1[mt][0];
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
             xslot_issue<KPW>(A, s0 + t + (uint32_t)D, t + (uint32_t)D < nst, cw, ln, ring[d]);
             __builtin_amdgcn_sched_barrier(0);
+            if (d % R != R - 1) continue;  // the group's partials meet after its last strip
+            const uint32_t tg = t + 1u - (uint32_t)R;  // first strip of the group
 #if NF4_XR_DEBUG == 1
-            if (live && wave == 0) {
-                float* h = held + t * (16u * MT * 16u) + 4u * kh * 16u + nl;
+            if (tg < nst && wave == 0) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) h[16u * r] = acc[0][0][r];
+                for (int r = 0; r < R; ++r) {
+                    if (tg + r >= nst) break;
+                    float* h = held + (tg + r) * (16u * MT * 16u) + 4u * kh * 16u + nl;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) h[16u * q] = accs[r][0][q];
+                }
             }
             if (false) {
 #else
-            if (live) {
+            if (tg < nst) {  // uniform
 #endif
-                f32x4* rb = red + (t & 1u) * (WV * MT * 64);
+                // red slot of strip u: ((u / R) & 1) * R + u % R (two groups in flight)
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) rb[(wave * MT + mt) * 64 + lane] = acc[mt][0];
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t u = tg + (uint32_t)r;
+                    if (u < nst) {
+                        f32x4* rb = red + (((u / R) & 1u) * R + (uint32_t)r) * (WV * MT * 64);
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt) rb[(wave * MT + mt) * 64 + lane] = accs[r][mt];
+                    }
+                }
                 __syncthreads();
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    if (wave == (t * MT + (uint32_t)mt) % (uint32_t)WV) {  // uniform
-                        f32x4 sum = rb[mt * 64 + lane];
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t u = tg + (uint32_t)r;
+                    const f32x4* rb = red + (((u / R) & 1u) * R + (uint32_t)r) * (WV * MT * 64);
 #pragma unroll
-                        for (int w = 1; w < WV; ++w) sum += rb[(w * MT + mt) * 64 + lane];
-                        // sum[r] = Y[16 mt + 4 kh + r][strip col nl]
-                        float* h = held + t * (16u * MT * 16u) + (16u * mt + 4u * kh) * 16u + nl;
+                    for (int mt = 0; mt < MT; ++mt) {
+                        if (u < nst && wave == (u * MT + (uint32_t)mt) % (uint32_t)WV) {  // uniform
+                            f32x4 sum = rb[mt * 64 + lane];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) h[16u * r] = sum[r];
+                            for (int w = 1; w < WV; ++w) sum += rb[(w * MT + mt) * 64 + lane];
+                            // sum[q] = Y[16 mt + 4 kh + q][strip col nl]
+                            float* h = held + u * (16u * MT * 16u) + (16u * mt + 4u * kh) * 16u + nl;
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) h[16u * q] = sum[q];
+                        }
                     }
                 }
             }
@@ -1961,8 +1982,9 @@ static int launch_xs(const HostMat* mats, int count, const void* x, int64_t M, i
 // (ticket flags) and within LDS.
 static uint32_t xr_lds_bytes(int64_t M, int waves, int kpw, uint32_t T) {
     const uint32_t mt = M > 16 ? 2u : 1u;
+    const uint32_t r = waves == 8 ? 2u : 1u;  // strips per reduction group (kernel's R; depth is even)
     const uint32_t tables = kpw == 2 ? 256u * 32u * 8u + 1024u : 0u;  // pair table + q/127 (256-deep chunks)
-    return tables + 2u * (uint32_t)waves * mt * 1024u + 64u + 256u + T * mt * 1024u;  // partials, codes, flags, held
+    return tables + 2u * r * (uint32_t)waves * mt * 1024u + 64u + 256u + T * mt * 1024u;  // partials, codes, flags, held
 }
 
 static uint32_t xr_per_wg(int64_t M, int64_t strips, const nf4_gemm_cfg& c) {
