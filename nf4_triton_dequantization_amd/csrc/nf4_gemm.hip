@@ -583,14 +583,34 @@ struct XLane {
     uint32_t b2;  // nl * groups
 };
 
+// The weight the ring is issuing from, kept in scalar registers: the strips of a
+// workgroup rarely cross into the next weight of a group, so the descriptor loads
+// (scalar memory, waited for before the refill's first vector load) happen once per
+// weight, not once per strip.
+struct XMat {
+    __amdgpu_buffer_rsrc_t rw, ra1, ra2;
+    FastDiv nb, n2;
+    uint32_t begin, next;  // [begin, next): the cached weight's strips in the launch
+};
+
+__device__ __forceinline__ void xmat_load(const GemmArgs& A, uint32_t strip, XMat& m) {
+    const uint32_t mi = xr_mat_of(A, strip);
+    const K128Mat& Mt = A.mat[mi];
+    m.rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);
+    m.ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a1, 0, Mt.nb.d, kRsrcFlags);
+    m.ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a2, 0, Mt.n2.d * 4u, kRsrcFlags);
+    m.nb = Mt.nb;
+    m.n2 = Mt.n2;
+    m.begin = Mt.cg_begin;
+    m.next = mi + 1u < A.nmat ? A.mat[mi + 1u].cg_begin : 0xFFFFFFFFu;
+}
+
 template <int KPW>
 __device__ __forceinline__ void xslot_issue(const GemmArgs& A, uint32_t strip, bool valid, uint32_t cw,
-                                            const XLane& ln, XSlot<KPW>& s) {
-    const K128Mat& Mt = A.mat[xr_mat_of(A, strip)];
-    const uint32_t r0 = (strip - Mt.cg_begin) * 16u;  // first row of the strip (uniform)
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);
-    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a1, 0, Mt.nb.d, kRsrcFlags);
-    const __amdgpu_buffer_rsrc_t ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a2, 0, Mt.n2.d * 4u, kRsrcFlags);
+                                            const XLane& ln, XMat& Mt, XSlot<KPW>& s) {
+    if (strip >= Mt.next) xmat_load(A, strip, Mt);  // uniform; scalar loads only
+    const uint32_t r0 = (strip - Mt.begin) * 16u;  // first row of the strip (uniform)
+    const __amdgpu_buffer_rsrc_t rw = Mt.rw, ra1 = Mt.ra1, ra2 = Mt.ra2;
     // invalid (past the strips or past K): offsets beyond every range -- zeros, no
     // traffic, and still one counted load each (a straight-line ring)
     const uint32_t oob = valid && cw + (uint32_t)(KPW - 1) < A.chunks ? 0u : kOob;
@@ -711,9 +731,11 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
         }
     __builtin_amdgcn_sched_barrier(0);  // issue order = wait order: x, then the ring slot by slot
     XSlot<KPW> ring[D];
+    XMat xm;
+    xmat_load(A, s0, xm);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        xslot_issue<KPW>(A, s0 + (uint32_t)d, (uint32_t)d < nst, cw, ln, ring[d]);
+        xslot_issue<KPW>(A, s0 + (uint32_t)d, (uint32_t)d < nst, cw, ln, xm, ring[d]);
         __builtin_amdgcn_sched_barrier(0);
     }
     write_lut(lut);
@@ -768,7 +790,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
-            xslot_issue<KPW>(A, s0 + t + (uint32_t)D, t + (uint32_t)D < nst, cw, ln, ring[d]);
+            xslot_issue<KPW>(A, s0 + t + (uint32_t)D, t + (uint32_t)D < nst, cw, ln, xm, ring[d]);
             __builtin_amdgcn_sched_barrier(0);
             if (d % R != R - 1) continue;  // the group's partials meet after its last strip
             const uint32_t tg = t + 1u - (uint32_t)R;  // first strip of the group
