@@ -2189,6 +2189,8 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     }
     if (!valid_gemm_cfg(cfg, M, N, K)) return NF4DQ_ERR_ARG;
     const size_t need = workspace_for(M, N, K, cfg);
+    // the kernels address the split-K slab through one buffer descriptor (32-bit range)
+    if (need >= (size_t(1) << 32)) return NF4DQ_ERR_TOO_LARGE;
     if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
     if (cfg.kernel == NF4DQ_GEMM_STREAM || cfg.kernel == NF4DQ_GEMM_PERSIST) {
         const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
@@ -2250,6 +2252,7 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
     }
     if (M * K * 2 >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
     const size_t need = cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
+    if (need >= (size_t(1) << 32)) return NF4DQ_ERR_TOO_LARGE;  // one buffer descriptor over the slab
     if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
     HostMat h[NF4DQ_GEMM_GROUP_MAX];
     for (int i = 0; i < count; ++i)
