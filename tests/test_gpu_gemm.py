@@ -43,8 +43,11 @@ def _x_bits(M, K, dt, seed):
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("M,N,K", [(1, 64, 128), (3, 128, 512), (16, 256, 1024), (17, 192, 384), (32, 64, 4096),
-                                   (1, 4096, 4096), (8, 1024, 4096), (4, 512, 11008), (2, 448, 14336)])
+                                   (1, 4096, 4096), (8, 1024, 4096), (4, 512, 11008), (2, 448, 14336),
+                                   (24, 2048, 4096), (32, 4096, 1280), (17, 2112, 14336)])
 def test_fused_gemm_vs_float64_oracle(coracle, gpu, dt, M, N, K):
+    # the last three take the library's register-resident choice (16 < M <= 32,
+    # N >= 2048, K % 256 == 0): two K slices, one slice with idle waves, seven slices
     from nf4_triton_dequantization_amd import nf4_linear
 
     packed, a1, a2 = O.make_inputs(N, K, seed=M * 7 + N + K, a2_kind="normal")
