@@ -192,7 +192,7 @@ __device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rs
 template <int DT, int MODE, int U, int AUXS, int X4 = 0>
 __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_t ro, const float* lut,
                                             const TileIn<U>& in_, uint32_t base, uint32_t lane,
-                                            uint32_t* stage = nullptr) {
+                                            uint32_t* stage = nullptr, const float* code2s = nullptr) {
     TileIn<U> in = in_;
     if constexpr (X4) {
         // lane l holds packed bytes [16l, 16l+16); the store layout wants dword
@@ -206,7 +206,9 @@ __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_
     if constexpr (MODE == kRef) {
         s = ((float)in.a1 / 127.0f) * in.a2;  // IEEE division (:45, :270), then fp32 multiply
     } else if constexpr (MODE == kBnb) {
-        s = D.code2[in.a1] * in.a2 + D.offset;
+        // the 256-entry code from the workgroup's LDS copy: a global gather here
+        // would wait on the absmax byte and then on L2 again, once per tile
+        s = code2s[in.a1] * in.a2 + D.offset;
     } else {
         s = in.a2;
     }
@@ -291,6 +293,7 @@ __device__ __forceinline__ void make_rsrcs(const Batch<MAXB>& bt, uint32_t k, __
 template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB, int X4 = 0>
 __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt) {
     __shared__ __attribute__((aligned(16))) float lut[16];
+    __shared__ __attribute__((aligned(16))) float code2s[MODE == kBnb ? 256 : 1];  // bitsandbytes code (every piece's)
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[X4 ? WPG * 256 : 1];
     uint32_t* stage = stage_all + (X4 ? (threadIdx.x >> 6) * 256 : 0);
     const uint32_t lane = threadIdx.x & 63u;
@@ -322,6 +325,9 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
         for (int j = 0; j < kStores; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, roa, 0xFFFFF000u + 16u * j, 0, AUXS);
     }
     write_lut(lut);
+    if constexpr (MODE == kBnb) {  // every piece of a bitsandbytes stream carries the same code
+        for (uint32_t i = threadIdx.x; i < 256u; i += 64u * WPG) code2s[i] = bt.d[0].code2[i];
+    }
     __syncthreads();
     if (!ca.valid) {
         NF4_FSTAMP(0, t_entry);
@@ -335,7 +341,7 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
         __amdgpu_buffer_rsrc_t rpb = rpa, rob = roa;
         if (MAXB > 1 && cb.k != ca.k) make_rsrcs<DT>(bt, cb.k, rpb, rob);
         const TileIn<U> B = tile_load<DT, MODE, U, AUXL, X4>(bt.d[cb.k], rpb, cb.base, lane);
-        tile_finish<DT, MODE, U, AUXS, X4>(bt.d[ca.k], roa, lut, A, ca.base, lane, stage);
+        tile_finish<DT, MODE, U, AUXS, X4>(bt.d[ca.k], roa, lut, A, ca.base, lane, stage, code2s);
 #if NF4_FLAT_STAMPS
         if (tiles_done == 0) NF4_FSTAMP(1, NF4_FNOW());
         ++tiles_done;
@@ -346,7 +352,7 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
         __amdgpu_buffer_rsrc_t rpn = rpb, ron = rob;
         if (MAXB > 1 && cn.k != cb.k) make_rsrcs<DT>(bt, cn.k, rpn, ron);
         A = tile_load<DT, MODE, U, AUXL, X4>(bt.d[cn.k], rpn, cn.base, lane);
-        tile_finish<DT, MODE, U, AUXS, X4>(bt.d[cb.k], rob, lut, B, cb.base, lane, stage);
+        tile_finish<DT, MODE, U, AUXS, X4>(bt.d[cb.k], rob, lut, B, cb.base, lane, stage, code2s);
 #if NF4_FLAT_STAMPS
         ++tiles_done;
 #endif
