@@ -183,10 +183,12 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
 #define NF4DQ_GEMM_XS 4
 /* NF4DQ_GEMM_XR: register-resident activation kernel (any M <= 32, K % 128 ==
  * 0): the K split is over the `waves` (8/16) waves of a workgroup, each holding
- * its x fragments of `strips` (1/2) 128-deep chunks in registers for the whole
+ * its x fragments of `strips` 128-deep chunks in registers for the whole
  * launch; a workgroup walks its column strips with a `depth` (2/4) deep ring of
- * weight loads and sums the waves' partial tiles in LDS; ksplit must equal
- * ceil(K/128 / (waves * strips)) (1 = no cross-workgroup reduction). */
+ * weight loads and sums the waves' partial tiles in LDS; `strips` = 128-deep
+ * chunks per wave: 1, 2 (one 256-deep chunk, K % 256 == 0) or 4 (two, 8 waves
+ * only, K % 512 == 0); ksplit must equal ceil(K/128 / (waves * strips))
+ * (1 = no cross-workgroup reduction). */
 #define NF4DQ_GEMM_XR 5
 typedef struct nf4_gemm_cfg {
     int32_t kernel;

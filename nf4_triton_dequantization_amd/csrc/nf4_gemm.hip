@@ -556,12 +556,14 @@ __global__ __launch_bounds__(64 * WV, 4) void nf4_gemm_xs_kernel(const GemmArgs 
 // so the weights entering the MFMAs are exactly nf4_dequant_ref's.
 // KPW = 1: one 128-deep chunk per wave (lane: 16 B of its row); KPW = 2: one
 // 256-deep chunk (lane: 32 contiguous bytes = one 64-block, so a wave's loads
-// cover whole 128-byte lines of its 16 rows, and one scale per lane).
+// cover whole 128-byte lines of its 16 rows, and one scale per lane); KPW = 4:
+// two consecutive 256-deep chunks (8 waves then span K = 4096 without a K split).
 template <int KPW>
 struct XSlot {
+    static constexpr int NSC = KPW == 4 ? 2 : 1;  // 64-blocks (scales) per lane: one per 256-deep sub-chunk
     u32x4 w[KPW];
-    uint8_t qa;  // kept 8-bit: a widening right after the load would wait for it (a drained ring)
-    float qb;
+    uint8_t qa[NSC];  // kept 8-bit: a widening right after the load would wait for it (a drained ring)
+    float qb[NSC];
 };
 
 // The weight owning a strip: straight-line selects over the group (no loop in
@@ -611,24 +613,31 @@ __device__ __forceinline__ void xslot_issue(const GemmArgs& A, uint32_t strip, b
     if (strip >= Mt.next) xmat_load(A, strip, Mt);  // uniform; scalar loads only
     const uint32_t r0 = (strip - Mt.begin) * 16u;  // first row of the strip (uniform)
     const __amdgpu_buffer_rsrc_t rw = Mt.rw, ra1 = Mt.ra1, ra2 = Mt.ra2;
-    // invalid (past the strips or past K): offsets beyond every range -- zeros, no
-    // traffic, and still one counted load each (a straight-line ring)
-    const uint32_t oob = valid && cw + (uint32_t)(KPW - 1) < A.chunks ? 0u : kOob;
-    // the lane's block: 2 cw + kh/2 (KPW 1) / 4 (cw/2) + kh = 2 cw + kh (KPW 2); its
-    // nested group (block / 4) is cw / 2 either way (uniform)
-    const uint32_t w0 = r0 * (A.K >> 1) + cw * 64u + ln.w;
+    constexpr int NSC = XSlot<KPW>::NSC;
 #pragma unroll
-    for (int q = 0; q < KPW; ++q) s.w[q] = __builtin_amdgcn_raw_buffer_load_b128(rw, (w0 + 16u * q) | oob, 0, 0);
+    for (int h = 0; h < NSC; ++h) {
+        const uint32_t c = cw + 2u * (uint32_t)h;  // first 128-deep chunk of this sub-chunk
+        // invalid (past the strips or past K): offsets beyond every range -- zeros, no
+        // traffic, and still one counted load each (a straight-line ring)
+        const uint32_t oob = valid && c + (KPW == 1 ? 0u : 1u) < A.chunks ? 0u : kOob;
+        // the lane's block: 2c + kh/2 (KPW 1) / 4 (c/2) + kh = 2c + kh (256-deep); its
+        // nested group (block / 4) is c / 2 either way (uniform)
+        const uint32_t w0 = r0 * (A.K >> 1) + c * 64u + ln.w;
+        constexpr int WQ = KPW == 1 ? 1 : 2;  // 16-byte weight loads per sub-chunk
+#pragma unroll
+        for (int q = 0; q < WQ; ++q)
+            s.w[WQ * h + q] = __builtin_amdgcn_raw_buffer_load_b128(rw, (w0 + 16u * q) | oob, 0, 0);
 #if NF4_XR_DEBUG == 2
-    s.qa = (uint8_t)(fmodu(r0 * A.bpr + 2u * cw + ln.b1, Mt.nb) | 1u);
-    s.qb = __uint_as_float(0x3c000000u | (fmodu(r0 * A.groups + (cw >> 1) + ln.b2, Mt.n2) & 0xFFu));
-    (void)ra1;
-    (void)ra2;
+        s.qa[h] = (uint8_t)(fmodu(r0 * A.bpr + 2u * c + ln.b1, Mt.nb) | 1u);
+        s.qb[h] = __uint_as_float(0x3c000000u | (fmodu(r0 * A.groups + (c >> 1) + ln.b2, Mt.n2) & 0xFFu));
+        (void)ra1;
+        (void)ra2;
 #else
-    s.qa = __builtin_amdgcn_raw_buffer_load_b8(ra1, fmodu(r0 * A.bpr + 2u * cw + ln.b1, Mt.nb) | oob, 0, 0);  // (:173-177)
-    s.qb = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-        ra2, (fmodu(r0 * A.groups + (cw >> 1) + ln.b2, Mt.n2) * 4u) | oob, 0, 0));  // (:40-41, :183-186)
+        s.qa[h] = __builtin_amdgcn_raw_buffer_load_b8(ra1, fmodu(r0 * A.bpr + 2u * c + ln.b1, Mt.nb) | oob, 0, 0);  // (:173-177)
+        s.qb[h] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            ra2, (fmodu(r0 * A.groups + (c >> 1) + ln.b2, Mt.n2) * 4u) | oob, 0, 0));  // (:40-41, :183-186)
 #endif
+    }
 }
 
 // Dequant + MFMA of one 256-deep chunk with the activations in registers (KPW = 2):
@@ -692,8 +701,8 @@ __device__ __forceinline__ void xr_pair_mma(const u32x4& w0, const u32x4& w1, fl
 template <int DT, int MT, int WV, int KPW, int D>
 __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) {
     extern __shared__ __attribute__((aligned(16))) f32x4 xr_smem[];  // all LDS dynamic (host: xr_lds_bytes)
-    // KPW = 2: the pair table (64 KiB) and the q/127 table lead the region
-    constexpr int kPt = KPW == 2 ? (256 * 32 * 8 + 1024) / 16 : 0;  // in f32x4
+    // 256-deep chunks: the pair table (64 KiB) and the q/127 table lead the region
+    constexpr int kPt = KPW >= 2 ? (256 * 32 * 8 + 1024) / 16 : 0;  // in f32x4
     f32x2* ptab = reinterpret_cast<f32x2*>(xr_smem);
     float* qtab = reinterpret_cast<float*>(xr_smem + (256 * 32 * 8) / 16);
     // partial tiles meet once per R strips (8 waves: two strips per barrier)
@@ -711,7 +720,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     const uint32_t s1 = s0 + T < A.col_groups ? s0 + T : A.col_groups;
     const uint32_t nst = s1 > s0 ? s1 - s0 : 0u;
     const uint32_t cw = (ks * (uint32_t)WV + wave) * (uint32_t)KPW;  // the wave's first chunk
-    const XLane ln{nl * (A.K >> 1) + (KPW == 2 ? 32u : 16u) * kh, nl * A.bpr + (KPW == 2 ? kh : kh >> 1),
+    const XLane ln{nl * (A.K >> 1) + (KPW >= 2 ? 32u : 16u) * kh, nl * A.bpr + (KPW >= 2 ? kh : kh >> 1),
                    nl * A.groups};
 
     // 1. the wave's x fragments (rows >= M and chunks past K read as zeros),
@@ -722,10 +731,13 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     for (int q = 0; q < KPW; ++q)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-            // k of fragment (q, s): cw 128 + 32 KPW kh + 32 q + 8 s -- the weight dword's k (same permutation)
+            // k of fragment (q, s): 128 cw + 32 kh + 8 s (KPW 1), 128 cw + 256 (q / 2) + 64 kh
+            // + 32 (q % 2) + 8 s (256-deep sub-chunks) -- the weight dword's k (same permutation)
             const uint32_t r = 16u * mt + nl;
-            const uint32_t xoff = r < A.M && cw + (uint32_t)(KPW - 1) < A.chunks
-                                      ? (r * A.K + cw * kChunkK + 32u * KPW * kh + 32u * q) * 2u : kOob;
+            const uint32_t c = cw + (KPW == 1 ? 0u : 2u * (uint32_t)(q / 2));
+            const uint32_t xoff = r < A.M && c + (KPW == 1 ? 0u : 1u) < A.chunks
+                                      ? (r * A.K + c * kChunkK + (KPW == 1 ? 32u : 64u) * kh + 32u * (q % 2)) * 2u
+                                      : kOob;
 #pragma unroll
             for (int s = 0; s < 4; ++s) xf[q][mt][s] = __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + 16u * s, 0, 0);
         }
@@ -739,7 +751,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
         __builtin_amdgcn_sched_barrier(0);
     }
     write_lut(lut);
-    if constexpr (KPW == 2) {  // tables while the loads fly (as the streaming kernels)
+    if constexpr (KPW >= 2) {  // tables while the loads fly (as the streaming kernels)
         if (tid < 256u) qtab[tid] = (float)tid / 127.0f;  // IEEE division (:45)
         for (uint32_t u = tid; u < 16u * 32u; u += 64u * WV) {
             const float clo = nf4_code(u >> 5);
@@ -765,18 +777,23 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
             if (live) {
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if constexpr (KPW == 2 && NF4_XR_DEBUG != 4) {
-                    xr_pair_mma<DT, MT>(ring[d].w[0], ring[d].w[1], qtab[ring[d].qa] * ring[d].qb, ptab, slot8, xf, acc);
+                if constexpr (KPW >= 2 && NF4_XR_DEBUG != 4) {
+#pragma unroll
+                    for (int h = 0; h < KPW / 2; ++h) {
+                        const u32x4 (&xs)[2][MT][4] = *reinterpret_cast<const u32x4 (*)[2][MT][4]>(&xf[2 * h]);
+                        xr_pair_mma<DT, MT>(ring[d].w[2 * h], ring[d].w[2 * h + 1],
+                                            qtab[ring[d].qa[h]] * ring[d].qb[h], ptab, slot8, xs, acc);
+                    }
                 }
 #pragma unroll
-                for (int q = 0; q < (KPW == 2 && NF4_XR_DEBUG != 4 ? 0 : KPW); ++q) {
+                for (int q = 0; q < (KPW >= 2 && NF4_XR_DEBUG != 4 ? 0 : KPW); ++q) {
                     Chunk<MT, 1> ch;
                     ch.w[0] = ring[d].w[q];
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                         for (int s = 0; s < 4; ++s) ch.x[mt][s] = xf[q][mt][s];
-                    const float scs[1] = {((float)ring[d].qa / 127.0f) * ring[d].qb};  // IEEE division (:45)
+                    const float scs[1] = {((float)ring[d].qa[q / 2] / 127.0f) * ring[d].qb[q / 2]};  // IEEE division (:45)
                     f32x4 a1[MT][1];
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) a1[mt][0] = acc[mt];
@@ -1665,10 +1682,12 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
     if (c.kernel == NF4DQ_GEMM_XR) {
         if (c.waves != 8 && c.waves != 16) return false;
         if (c.depth != 2 && c.depth != 4) return false;
-        if (c.strips != 1 && c.strips != 2) return false;  // 128-deep chunks per wave
+        if (c.strips != 1 && c.strips != 2 && c.strips != 4) return false;  // 128-deep chunks per wave
+        if (c.strips == 4 && (c.waves != 8 || K % 512)) return false;          // two 256-deep chunks per wave
+        if (c.strips == 4 && c.depth == 4 && M > 16) return false;             // 64 x VGPRs + a 4-deep ring spill
         // x + a 4-deep ring spill within 16 waves' 128 registers (8 waves: 256)
         if (M > 16 && c.strips == 2 && c.depth == 4 && c.waves == 16) return false;
-        if (c.strips == 2 && K % 256) return false;                 // 256-deep chunks
+        if (c.strips >= 2 && K % 256) return false;                 // 256-deep chunks
         const int64_t chunks = K / kChunkK, per = (int64_t)c.waves * c.strips;
         return c.ksplit == (chunks + per - 1) / per && c.ksplit <= 1024;
     }
@@ -2005,12 +2024,12 @@ static int launch_xs(const HostMat* mats, int count, const void* x, int64_t M, i
 static uint32_t xr_lds_bytes(int64_t M, int waves, int kpw, uint32_t T) {
     const uint32_t mt = M > 16 ? 2u : 1u;
     const uint32_t r = waves == 8 ? 2u : 1u;  // strips per reduction group (kernel's R; depth is even)
-    const uint32_t tables = kpw == 2 ? 256u * 32u * 8u + 1024u : 0u;  // pair table + q/127 (256-deep chunks)
+    const uint32_t tables = kpw >= 2 ? 256u * 32u * 8u + 1024u : 0u;  // pair table + q/127 (256-deep chunks)
     return tables + 2u * r * (uint32_t)waves * mt * 1024u + 64u + 256u + T * mt * 1024u;  // partials, codes, flags, held
 }
 
 static uint32_t xr_per_wg(int64_t M, int64_t strips, const nf4_gemm_cfg& c) {
-    const uint32_t wg_per_cu = c.waves == 16 || c.strips == 2 ? 1u : 2u;  // the pair table leaves room for one
+    const uint32_t wg_per_cu = c.waves == 16 || c.strips >= 2 ? 1u : 2u;  // the pair table leaves room for one
     uint32_t P = (uint32_t)device_cus() * wg_per_cu / (uint32_t)c.ksplit;  // workgroups per K slice
     if (P < 1) P = 1;
     uint32_t T = (uint32_t)((strips + P - 1) / P);
@@ -2074,10 +2093,11 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
         if (cfg.strips == 2) NF4_RD(DT_, MT_, W_, 2); \
         else NF4_RD(DT_, MT_, W_, 1);                 \
     } while (0)
-#define NF4_RW(DT_, MT_)                          \
-    do {                                          \
-        if (cfg.waves == 16) NF4_RK(DT_, MT_, 16); \
-        else NF4_RK(DT_, MT_, 8);                 \
+#define NF4_RW(DT_, MT_)                                \
+    do {                                                \
+        if (cfg.strips == 4) NF4_RD(DT_, MT_, 8, 4);    \
+        else if (cfg.waves == 16) NF4_RK(DT_, MT_, 16); \
+        else NF4_RK(DT_, MT_, 8);                       \
     } while (0)
 #define NF4_RM(DT_)                 \
     do {                            \

@@ -558,9 +558,10 @@ def test_register_resident_kernel_vs_oracle(coracle, gpu, dt, M, N, K):
     ran = 0
     for waves in (8, 16):
         for depth in (2, 4):
-            for kpw in (1, 2):
+            for kpw in (1, 2, 4):
                 cfg = _xr_cfg(_lib, K, waves, depth, kpw)
-                if (M > 16 and kpw == 2 and depth == 4 and waves == 16) or (kpw == 2 and K % 256):
+                if ((M > 16 and kpw == 2 and depth == 4 and waves == 16) or (kpw == 2 and K % 256)
+                        or (kpw == 4 and (waves != 8 or K % 512 or (M > 16 and depth == 4)))):
                     assert _gemm_cfg_call(L, _lib, x, t, y, code, N, K, cfg) == _lib.ERR_ARG
                     continue
                 for _ in range(2):  # twice: the tickets the first call left at 0 are reused
@@ -572,7 +573,8 @@ def test_register_resident_kernel_vs_oracle(coracle, gpu, dt, M, N, K):
                     except AssertionError as e:
                         raise AssertionError(f"cfg waves={waves} depth={depth} kpw={kpw}: {e}") from None
                 ran += 1
-    assert ran == (4 if K % 256 else 7 if M > 16 else 8)
+    kpw4 = 0 if K % 512 else (1 if M > 16 else 2)  # 8 waves only; a 4-deep ring only up to 16 rows
+    assert ran == (4 if K % 256 else 7 if M > 16 else 8) + kpw4
     bad = _lib.GemmCfg(_lib.GEMM_XR, 16, 2, -(-(K // 128) // 16) + 1, 1)  # ksplit must be ceil(chunks / 16)
     assert _gemm_cfg_call(L, _lib, x, t, y, code, N, K, bad) == _lib.ERR_ARG
 
@@ -609,7 +611,7 @@ def test_register_resident_kernel_grouped(coracle, gpu, wrap, M):
                                tt[2].numel(), y.data_ptr(), N)
     xt, xb = _x_bits(M, K, "bf16", seed=67 + M)
     x = xt.to(gpu)
-    for waves, depth, kpw in ((16, 4, 1), (16, 2, 2), (8, 2, 1), (8, 4, 1)):
+    for waves, depth, kpw in ((16, 4, 1), (16, 2, 2), (8, 2, 1), (8, 4, 1), (8, 2, 4)):
         c = _xr_cfg(_lib, K, waves, depth, kpw)
         wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, mats, len(Ns), ctypes.byref(c))
         ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=gpu)

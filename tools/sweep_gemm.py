@@ -94,7 +94,7 @@ def main():
                     cfgs.append(_lib.GemmCfg(_lib.GEMM_XS, waves, kc, -(-(k // 128) // kc), 1))
             for waves in (8, 16):
                 for depth in (2, 4):
-                    for kpw in (1, 2):  # register-resident kernel: chunks per wave; ksplit follows
+                    for kpw in (1, 2, 4):  # register-resident kernel: chunks per wave; ksplit follows
                         cfgs.append(_lib.GemmCfg(_lib.GEMM_XR, waves, depth, -(-(k // 128) // (waves * kpw)), kpw))
             cfgs = [c for c in cfgs if c.kernel in kern]
             for cfg in cfgs:

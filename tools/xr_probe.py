@@ -34,7 +34,7 @@ def main():
         ref = x.float() @ W.float().t()
         for waves in (8, 16):
             for depth in (2, 4):
-                for kpw in (1, 2):
+                for kpw in (1, 2, 4):
                     ks = -(-(K // 128) // (waves * kpw))
                     cfg = _lib.GemmCfg(_lib.GEMM_XR, waves, depth, ks, kpw)
                     wsz = L.nf4_gemm_workspace_bytes_cfg(M, N, K, ctypes.byref(cfg))
@@ -46,6 +46,7 @@ def main():
                     torch.cuda.synchronize()
                     if rc:
                         print(json.dumps({"M": M, "N": N, "K": K, "cfg": [waves, depth, ks, kpw], "rc": rc}))
+                        torch.cuda.synchronize()
                         continue
                     err = ((y.float() - ref).abs() / (ref.abs() + 1.0)).nan_to_num(1e9)
                     bad = (err > 0.02).nonzero()
