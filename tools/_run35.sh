@@ -1,0 +1,8 @@
+# register-resident GEMM today: product vs no-LDS-reduction (xr1) vs no dequant/MFMA (xr3) at M = 1, 32 on 14336x4096
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/r35 && export TMPDIR=/tmp
+O=gpurun_out/r35
+for v in prod 1 3; do
+  if [ $v = prod ]; then unset NF4DQ_LIB_PATH; else export NF4DQ_LIB_PATH=$PWD/tools/_diag/diag_xr$v.so; fi
+  timeout -k 10 300 python -u tools/sweep_gemm.py --ms 1,32 --kernels 5 --shapes "14336,4096;4096,14336" > $O/sweep_$v.jsonl 2> $O/sweep_$v.err || exit 1
+done
+echo ALLDONE
