@@ -101,9 +101,16 @@ def load_nf4_safetensors(path: str, device="cpu") -> Dict[str, Linear4bit]:
 
     tensors: Dict[str, torch.Tensor] = {}
     with safe_open(path, framework="pt", device="cpu") as f:
-        for k in f.keys():
-            tensors[k] = f.get_tensor(k)
-    prefixes = [k[: -len(QS_SUFFIX) - 1] for k in tensors if k.endswith("." + QS_SUFFIX)]
+        keys = list(f.keys())
+        prefixes = [k[: -len(QS_SUFFIX) - 1] for k in keys if k.endswith("." + QS_SUFFIX)]
+        # only the NF4 weights' entries are read (a checkpoint's other tensors --
+        # embeddings, norms, unquantized heads -- stay on disk)
+        wanted = set(prefixes)
+        wanted.update(f"{p}.{s}" for p in prefixes for s in
+                      ("absmax", "quant_map", "nested_absmax", "nested_quant_map", QS_SUFFIX))
+        for k in keys:
+            if k in wanted:
+                tensors[k] = f.get_tensor(k)
     out: Dict[str, Linear4bit] = {}
     for prefix in sorted(prefixes):
         qs = quant_state_from_tensors(prefix, tensors, device)

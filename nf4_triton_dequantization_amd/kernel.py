@@ -340,6 +340,13 @@ def dequantize_nf4_bnb(module) -> torch.Tensor:
     if numel == 0:
         return out
     bs = int(qs.blocksize)
+    with torch.cuda.device(q.device):  # the launch's device = the weight's (not the current one)
+        rc = _launch_bnb(q, qs, out, code, numel, bs)
+    _lib.check(rc, "nf4 bnb dequantize")
+    return out
+
+
+def _launch_bnb(q, qs, out, code, numel, bs) -> int:
     L = _lib.lib()
     stream = _stream_ptr(q.device)
     nested = getattr(qs, "state2", None) is not None and qs.absmax.dtype == torch.uint8
@@ -358,8 +365,7 @@ def dequantize_nf4_bnb(module) -> torch.Tensor:
         am = qs.absmax.to(torch.float32).contiguous().view(-1)
         rc = L.nf4_dequant_bnb_single(q.data_ptr(), am.data_ptr(), am.numel(), out.data_ptr(), code, numel,
                                       bs, stream)
-    _lib.check(rc, "nf4 bnb dequantize")
-    return out
+    return rc
 
 
 _GEMM_WS = {}

@@ -59,6 +59,52 @@ def test_roundtrip(tmp_path):
             assert q2.state2 is None
 
 
+def test_mixed_checkpoint_reads_only_nf4_entries(tmp_path, monkeypatch):
+    """A checkpoint also holding unquantized tensors (embeddings, norms): only the NF4
+    weights become modules, and only their entries are read from the file."""
+    from safetensors import safe_open
+    from safetensors.torch import save_file
+
+    from nf4_triton_dequantization_amd.checkpoint import quant_state_tensors
+
+    ws = _weights()
+    tensors = {}
+    for prefix, (packed, qs) in ws.items():
+        tensors.update(quant_state_tensors(prefix, packed, qs))
+    tensors["model.embed_tokens.weight"] = torch.randn(64, 32)
+    tensors["model.norm.weight"] = torch.ones(32)
+    path = str(tmp_path / "mixed.safetensors")
+    save_file(tensors, path)
+    read = []
+    real_open = safe_open
+
+    class _Spy:
+        def __init__(self, *a, **k):
+            self._f = real_open(*a, **k)
+
+        def __enter__(self):
+            self._f.__enter__()
+            return self
+
+        def __exit__(self, *exc):
+            return self._f.__exit__(*exc)
+
+        def keys(self):
+            return self._f.keys()
+
+        def get_tensor(self, k):
+            read.append(k)
+            return self._f.get_tensor(k)
+
+    import safetensors
+
+    monkeypatch.setattr(safetensors, "safe_open", _Spy)
+    mods = load_nf4_safetensors(path)
+    assert set(mods) == {k[: -len(".weight")] for k in ws}
+    assert "model.embed_tokens.weight" not in read and "model.norm.weight" not in read
+    assert set(read) == set(tensors) - {"model.embed_tokens.weight", "model.norm.weight"}
+
+
 @pytest.mark.gpu
 def test_loaded_checkpoint_dequantizes_on_gpu(tmp_path, coracle, gpu):
     from nf4_triton_dequantization import triton_dequantize_nf4
