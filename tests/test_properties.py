@@ -75,3 +75,58 @@ def test_generator_is_deterministic():
     b = O.golden_case_inputs(5, 77, 123, {"nb": 9, "n2": 2, "a2_kind": "normal"})
     for x, y in zip(a[:3], b[:3]):
         assert np.array_equal(x, y)
+
+
+# ---------------------------------------------------------------------------
+# bitsandbytes semantics (parity unpinned: bitsandbytes is
+# absent, so the numpy and C restatements check each other and the HIP path)
+# ---------------------------------------------------------------------------
+@st.composite
+def bnb_cases(draw):
+    bs = draw(st.sampled_from([64, 128, 256, 512, 1024, 4096]))
+    bs2 = draw(st.sampled_from([256, 256, 64, 1024]))
+    numel = draw(st.one_of(st.integers(1, 5000), st.sampled_from([64, 4096, 64 * 256 * 3, 64 * 1000 + 2])))
+    offset = draw(st.sampled_from([0.0, 0.03125, -1.5]))
+    dt = draw(st.sampled_from(["f16", "bf16", "f32"]))
+    seed = draw(st.integers(0, 2 ** 31 - 1))
+    return numel, bs, bs2, offset, dt, seed
+
+
+def _bnb_inputs(numel, bs, bs2, seed):
+    nblk = (numel + bs - 1) // bs
+    packed = O.splitmix64_bytes(seed, (numel + 1) // 2, stream=1)
+    a1 = O.splitmix64_bytes(seed, nblk, stream=2)
+    code2 = O.normal_f32(seed, 256, stream=5)
+    a2 = O.uniform_f32(seed, (nblk + bs2 - 1) // bs2, 1e-3, 1e-1, stream=3)
+    return packed, a1, code2, a2
+
+
+@settings(max_examples=80, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(bnb_cases())
+def test_bnb_restatements_agree(case):
+    numel, bs, bs2, offset, dt, seed = case
+    p, a1, code2, a2 = _bnb_inputs(numel, bs, bs2, seed)
+    code = DT_CODE[dt]
+    c = O.COracle().dequant_bnb(p, a1, code2, a2, offset, numel, code, bs, bs2)
+    assert_bits_equal(O.dequant_bnb_np(p, a1, code2, a2, offset, numel, code, bs, bs2), c, dt, f"numpy bnb {case}")
+
+
+@pytest.mark.gpu
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow,
+                                                                 HealthCheck.function_scoped_fixture])
+@given(bnb_cases())
+def test_bnb_hip_matches_c_oracle(gpu, case):
+    """The C ABI ``nf4_dequant_bnb`` on drawn sizes (ragged tails, every supported
+    blocksize, nested block sizes, offsets) against the C restatement, bit for bit."""
+    from nf4_triton_dequantization_amd import _lib
+
+    numel, bs, bs2, offset, dt, seed = case
+    p, a1, code2, a2 = _bnb_inputs(numel, bs, bs2, seed)
+    want = O.COracle().dequant_bnb(p, a1, code2, a2, offset, numel, DT_CODE[dt], bs, bs2)
+    t = [torch.from_numpy(v).to(gpu) for v in (p, a1, code2, a2)]
+    out = torch.empty(numel, dtype=torch_dtype(dt), device=gpu)
+    rc = _lib.lib().nf4_dequant_bnb(t[0].data_ptr(), t[1].data_ptr(), t[1].numel(), t[2].data_ptr(),
+                                    t[3].data_ptr(), t[3].numel(), offset, out.data_ptr(), DT_CODE[dt], numel,
+                                    bs, bs2, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, _lib.strerror(rc)
+    assert_bits_equal(out_bits(out), want, dt, f"hip bnb {case}")
