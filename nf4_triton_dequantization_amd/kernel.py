@@ -273,27 +273,41 @@ def reset_triton_dequantize_state() -> None:
     return None
 
 
-def dequantize_nf4_many(modules: Iterable) -> List[torch.Tensor]:
+def dequantize_nf4_many(modules: Iterable, out: Optional[Sequence[Optional[torch.Tensor]]] = None
+                        ) -> List[torch.Tensor]:
     """Dequantize several weights with as few launches as possible.
 
     Equivalent to ``[triton_dequantize_nf4(m) for m in modules]`` (the
     benchmark.py:68-84 pattern) but folds every uint8-absmax weight of one
     device and dtype into batched launches of up to ``NF4DQ_BATCH_MAX`` matrices.
+    ``out`` (optional, one entry per module, None = allocate): caller-owned
+    contiguous ``[out_features, in_features]`` tensors of ``quant_state.dtype`` on
+    the weight's device, written in place and returned (a preallocated weight
+    buffer reused across steps or graph replays).
     """
     modules = list(modules)
+    given = list(out) if out is not None else [None] * len(modules)
+    if len(given) != len(modules):
+        raise ValueError("dequantize_nf4_many: one out tensor (or None) per module")
     outs: List[Optional[torch.Tensor]] = [None] * len(modules)
     groups = {}
     keep = []  # tensors referenced by descriptors must outlive the launch
     for i, mod in enumerate(modules):
         qweight, absmax, absmax32, dtype, m, n = _prepare(mod)
+        o = given[i]
+        if o is not None and (o.shape != (m, n) or o.dtype != dtype or o.device != qweight.device
+                              or not o.is_contiguous()):
+            raise RuntimeError(f"dequantize_nf4_many: out[{i}] must be a contiguous {dtype} tensor of shape "
+                               f"({m}, {n}) on {qweight.device}")
         if qweight.device.type != "cuda" or absmax.dtype != torch.uint8 or dtype not in _DTYPE_CODE:
             # host tensors (NF4_BACKEND=cpu, or the reference's error), single-quant
             # absmax, fp64 output: one call each
-            outs[i] = triton_dequantize_nf4(mod)
+            r = triton_dequantize_nf4(mod)
+            outs[i] = o.copy_(r) if o is not None else r
             continue
         code = _dtype_code(dtype)
-        out = torch.empty((m, n), dtype=dtype, device=qweight.device)
-        outs[i] = out
+        out_t = o if o is not None else torch.empty((m, n), dtype=dtype, device=qweight.device)
+        outs[i] = out_t
         if m == 0 or n == 0:
             continue
         q = _as_u8_flat(qweight)
@@ -305,7 +319,7 @@ def dequantize_nf4_many(modules: Iterable) -> List[torch.Tensor]:
             raise ZeroDivisionError("integer division or modulo by zero (empty absmax)")
         keep.extend((q, a1, a2))
         d = _lib.MatrixDesc(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
-                            out.data_ptr(), m, n)
+                            out_t.data_ptr(), m, n)
         groups.setdefault((q.device, code), []).append(d)
     L = _lib.lib()
     for (device, code), descs in groups.items():

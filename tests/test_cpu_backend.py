@@ -151,3 +151,23 @@ def test_host_path_errors_and_many(cpu_backend):
     outs = dequantize_nf4_many(mods)
     for mod, o in zip(mods, outs):
         assert torch.equal(o, triton_dequantize_nf4(mod))
+
+
+def test_many_into_caller_outputs(cpu_backend):
+    """dequantize_nf4_many(out=...): caller-owned outputs written in place and returned;
+    a wrong shape / dtype / layout raises before anything runs."""
+    from nf4_triton_dequantization import triton_dequantize_nf4
+    from nf4_triton_dequantization_amd import dequantize_nf4_many
+
+    mods = [_module(*W.make_inputs(m, n, 60 + m), m, n, torch.bfloat16) for m, n in ((4, 128), (9, 256), (3, 64))]
+    bufs = [torch.full((4, 128), 7.0, dtype=torch.bfloat16), None, torch.empty((3, 64), dtype=torch.bfloat16)]
+    outs = dequantize_nf4_many(mods, out=bufs)
+    assert outs[0] is bufs[0] and outs[2] is bufs[2]
+    for mod, o in zip(mods, outs):
+        assert torch.equal(o, triton_dequantize_nf4(mod))
+    for bad in (torch.empty((4, 127), dtype=torch.bfloat16), torch.empty((4, 128), dtype=torch.float16),
+                torch.empty((128, 4), dtype=torch.bfloat16).t()):
+        with pytest.raises(RuntimeError, match="out\\[0\\]"):
+            dequantize_nf4_many(mods[:1], out=[bad])
+    with pytest.raises(ValueError):
+        dequantize_nf4_many(mods, out=bufs[:2])

@@ -169,6 +169,14 @@ def test_batched_matches_single_calls(coracle, gpu):
     torch.cuda.synchronize()
     for i, (o, w) in enumerate(zip(outs, wants)):
         assert_bits_equal(out_bits(o), w, "f16", f"batched #{i}")
+    # the same into caller-owned outputs (every other one preallocated, stale contents)
+    bufs = [torch.full((m, n), float("nan"), dtype=torch.float16, device=gpu) if i % 2 == 0 else None
+            for i, (m, n) in enumerate(shapes)]
+    outs = dequantize_nf4_many(mods, out=bufs)
+    torch.cuda.synchronize()
+    for i, (o, w) in enumerate(zip(outs, wants)):
+        assert bufs[i] is None or o is bufs[i]
+        assert_bits_equal(out_bits(o), w, "f16", f"batched into #{i}")
 
 
 @pytest.mark.parametrize("cfg", [(4, 0, 0, 0), (4, 0, 1, 0), (8, 0, 1, 0), (8, 2, 1, 1), (4, 1, 1, 1), (8, 8, 1, 0),
