@@ -661,5 +661,37 @@ try:
         y = nf4_linear(xt.to(gpu), mod)
         assert y.shape == (M, N)
         _check(y, xb, W, dt)
+    @st.composite
+    def _group_cases(draw):
+        M = draw(st.integers(1, 32))
+        K = draw(st.sampled_from([128, 384, 1024, 2048, 4096]))
+        Ns = draw(st.lists(st.integers(1, 40).map(lambda v: 64 * v), min_size=2, max_size=4))
+        wraps = draw(st.lists(st.booleans(), min_size=len(Ns), max_size=len(Ns)))
+        seed = draw(st.integers(0, 10 ** 6))
+        return M, K, Ns, wraps, seed
+
+    @settings(max_examples=30, deadline=None, suppress_health_check=[HealthCheck.too_slow,
+                                                                     HealthCheck.function_scoped_fixture])
+    @given(_group_cases())
+    def test_grouped_library_choice_property(coracle, gpu, case):
+        """Drawn weight groups (2-4 weights sharing x, some with absmax wrapping inside a
+        row) through nf4_linear_grouped -- one launch, the library's choice -- each output
+        against the float64 oracle."""
+        from nf4_triton_dequantization_amd import nf4_linear_grouped
+
+        M, K, Ns, wraps, seed = case
+        mods, Ws = [], []
+        for i, (N, wrap) in enumerate(zip(Ns, wraps)):
+            if wrap:
+                packed, a1, a2, _ = O.golden_case_inputs(N, K, seed + i, {"nb": 11 + i, "n2": 3, "a2_kind": "normal"})
+            else:
+                packed, a1, a2 = O.make_inputs(N, K, seed=seed + i, a2_kind="normal")
+            Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16))
+            mods.append(make_module(packed, a1, a2, N, K, "bf16", gpu))
+        xt, xb = _x_bits(M, K, "bf16", seed=seed % 997 + 3)
+        ys = nf4_linear_grouped(xt.to(gpu), mods)
+        for y, W, N in zip(ys, Ws, Ns):
+            assert y.shape == (M, N)
+            _check(y, xb, W, "bf16")
 except ImportError:  # hypothesis is part of the test environment; keep the module importable without it
     pass
