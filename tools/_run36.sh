@@ -1,5 +1,5 @@
 # register-resident GEMM with grouped reductions (one barrier pair per RG strips): parity, probe, sweep
-# (the grouped-reduction variant it measured was not kept: commit 96ff5c7 reverted the kernel; re-running this measures the product kernel)
+# (the grouped-reduction variant it measured was an uncommitted build, not kept -- see DESIGN §4b and commit 96ff5c7; re-running this measures the product kernel)
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/r36 && export TMPDIR=/tmp
 O=gpurun_out/r36
 timeout -k 10 600 python -u -m pytest tests/test_gpu_gemm.py -q -x --timeout 120 --timeout-method thread > $O/pytest_gemm.log 2>&1; rc=$?; tail -3 $O/pytest_gemm.log; [ $rc -eq 0 ] || exit $rc
