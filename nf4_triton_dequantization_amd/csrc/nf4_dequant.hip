@@ -194,7 +194,7 @@ __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_
                                             const TileIn<U>& in_, uint32_t base, uint32_t lane,
                                             uint32_t* stage = nullptr, const float* code2s = nullptr) {
     TileIn<U> in = in_;
-    if constexpr (X4) {
+    if constexpr (X4 == 1) {
         // lane l holds packed bytes [16l, 16l+16); the store layout wants dword
         // j of lane l = bytes [256j + 4l, +4).  One ds_write_b128 + four
         // ds_read_b32 on this wave's private 1 KiB slice (in-order per wave).
@@ -217,7 +217,9 @@ __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_
     constexpr uint32_t LB = lane_bytes<DT>();
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-        const uint32_t rel = 64u * LB * j + LB * lane;
+        // X4 == 2 (direct): dword j of lane l is packed bytes [16l + 4j, +4), stored
+        // where it came from (four 16 B stores per lane, each instruction strided by 64 B)
+        const uint32_t rel = X4 == 2 ? 16u * lane + 4u * j : 64u * LB * j + LB * lane;
         const float sj = __shfl(s, (int)(rel >> bsh), 64);
         const uint32_t w = in.w[j];
         const uint32_t hi4 = (w >> 2) & 0x3C3C3C3Cu;
@@ -534,6 +536,19 @@ int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_laun
     b.stamps = g_stamps;
 #endif
     const uint32_t pol = (uint32_t)((cfg.flags >> NF4DQ_CFG_STORE_POLICY_BIT) & 0xF);
+    if ((cfg.flags & (NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_X4_LOADS)) && (mode != kRef || dtype == NF4DQ_F32))
+        return NF4DQ_ERR_ARG;  // the 16 B/lane shapes: reference semantics, 16-bit outputs
+    if (cfg.flags & NF4DQ_CFG_X4_DIRECT) {  // 16 B/lane loads, strided 16 B stores: base shape only
+        if (U != 4 || wpg != 4 || !cfg.nontemporal || pol || (cfg.flags & NF4DQ_CFG_X4_LOADS)) return NF4DQ_ERR_ARG;
+        if (dtype == NF4DQ_BF16) {
+            if (ntl) launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, kAuxNt, 4, MAXB, 2>(b, blocks, st);
+            else launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, 0, 4, MAXB, 2>(b, blocks, st);
+        } else {
+            if (ntl) launch_one<NF4DQ_F16, kRef, 4, kAuxStore, kAuxNt, 4, MAXB, 2>(b, blocks, st);
+            else launch_one<NF4DQ_F16, kRef, 4, kAuxStore, 0, 4, MAXB, 2>(b, blocks, st);
+        }
+        return hip_rc(hipGetLastError());
+    }
     if (cfg.flags & NF4DQ_CFG_X4_LOADS) {  // 16 B/lane loads + LDS redistribution: base shape only
         if (U != 4 || wpg != 4 || !cfg.nontemporal || pol) return NF4DQ_ERR_ARG;
         if (dtype == NF4DQ_BF16) {
@@ -730,9 +745,9 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len, const uint8_t
                         const nf4_launch_cfg* cfg, void* hip_stream) {
     nf4_launch_cfg c = cfg ? *cfg : kDefaultCfg;
     if (c.tile_dwords != 1 && c.tile_dwords != 2 && c.tile_dwords != 4 && c.tile_dwords != 8) return NF4DQ_ERR_ARG;
-    if (c.tile_dwords < 4 && (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_STORE_POLICY_MASK)))
+    if (c.tile_dwords < 4 && (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_STORE_POLICY_MASK)))
         return NF4DQ_ERR_ARG;
-    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_SEG_SHIFT_MASK | NF4DQ_CFG_WG_SHIFT_MASK |
+    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_SEG_SHIFT_MASK | NF4DQ_CFG_WG_SHIFT_MASK |
                     NF4DQ_CFG_STORE_POLICY_MASK))
         return NF4DQ_ERR_ARG;
     if (((c.flags >> NF4DQ_CFG_SEG_SHIFT_BIT) & 0xF) > 6) return NF4DQ_ERR_ARG;

@@ -184,6 +184,7 @@ def test_batched_matches_single_calls(coracle, gpu):
                                  (8, 0, 1, 0x400), (4, 0, 1, 0x30), (8, 0, 1, 0x40), (4, 0, 1, 0x10),
                                  (4, 0, 0, 0x300), (8, 3, 1, 0x331), (4, 0, 1, 0x1000), (4, 0, 1, 0x5000), (4, 2, 1, 0x3100),
                                  (4, 0, 1, 0x2), (4, 1, 1, 0x3), (4, 0, 1, 0x302),
+                                 (4, 0, 1, 0x4), (4, 2, 1, 0x5), (4, 0, 1, 0x304),
                                  (2, 0, 1, 0), (2, 8, 1, 0), (1, 8, 1, 0), (2, 4, 1, 0x30), (1, 0, 1, 0)])
 def test_launch_configs_identical(coracle, gpu, cfg):
     from nf4_triton_dequantization_amd import _lib

@@ -3,6 +3,8 @@
 Times, with hipGraph replay over rotating buffers (>> 256 MiB Infinity Cache):
   * calib_mix  -- nf4_flat_kernel's exact load/store shapes, no decode
                   (1 B read : 4 B written, like NF4 -> 16-bit)
+  * calib_mix16 -- 16 B/lane loads (1 KiB per wave instruction), four strided 16 B
+                  stores per lane (the alternative tile shape)
   * nf4 dequant (bench default config) on the same sizes
   * calib_read / calib_write on 1 GiB (pure streams)
 Prints JSON lines: GB/s and fraction of the 8 TB/s spec.
@@ -67,12 +69,18 @@ def main():
                                       ctypes.c_void_p(outs[i % P].data_ptr()),
                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
 
+        def mix16(i):
+            assert C.calib_mix16_launch(ctypes.c_void_p(ins[i % P].data_ptr()), ctypes.c_uint32(nbytes),
+                                        ctypes.c_void_p(outs[i % P].data_ptr()),
+                                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+
         def deq(i):
             assert L.nf4_dequant_ref(ins[i % P].data_ptr(), nbytes, a1.data_ptr(), nb, a2.data_ptr(), a2.numel(),
                                      outs[i % P].data_ptr(), _lib.BF16, m, n,
                                      torch.cuda.current_stream().cuda_stream) == 0
 
         for name, fn, byt in (("calib_mix (same access shapes, no decode)", mix, nbytes * 5),
+                              ("calib_mix16 (16 B/lane loads, strided 16 B stores)", mix16, nbytes * 5),
                               ("nf4 dequant", deq, nbytes * 5 + nb + 4 * a2.numel())):
             t = graph_time(fn, 64)
             print(json.dumps({"kernel": name, "layout": layout, "m": m, "n": n, "us": t * 1e6,

@@ -74,3 +74,31 @@ extern "C" int calib_mix_launch(const void* p, uint32_t nbytes, void* o, void* s
                        (uint32_t*)o);
     return (int)hipGetLastError();
 }
+
+// Twin of a 16 B/lane load shape: lane l reads packed bytes tile+16l..+15 (one
+// 1 KiB-contiguous b128 load per wave) and writes its 64 output bytes as four b128
+// sc1+nt stores at 4*tile + 64l + 16s (each store instruction strided by 64 B; the
+// four together cover the wave's 4 KiB). Probes whether fewer, wider loads beat the
+// 4 B/lane shape of nf4_flat_kernel at one tile per wave.
+__global__ __launch_bounds__(256) void calib_mix16(const uint32_t* p, uint32_t nbytes, uint32_t* o) {
+    __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, nbytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)o, 0, nbytes * 4u, 0x00020000);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t base = wave * 1024u; base < nbytes; base += nw * 1024u) {
+        const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rp, base + 16u * lane, 0, 0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const u32x4 v = {w[s], w[s] ^ 1u, w[s] ^ 2u, w[s] ^ 3u};
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, (base + 16u * lane) * 4u + 16u * s, 0, 18);
+        }
+    }
+}
+
+extern "C" int calib_mix16_launch(const void* p, uint32_t nbytes, void* o, void* stream) {
+    const uint32_t tiles = (nbytes + 1023u) / 1024u;
+    hipLaunchKernelGGL(calib_mix16, dim3((tiles + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const uint32_t*)p,
+                       nbytes, (uint32_t*)o);
+    return (int)hipGetLastError();
+}
