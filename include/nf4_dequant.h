@@ -121,6 +121,7 @@ int nf4_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t n
 #define NF4DQ_CFG_NT_LOADS 1   /* nt cache policy on the packed-weight loads */
 #define NF4DQ_CFG_X4_LOADS 2   /* 16 B/lane packed loads, redistributed through LDS */
 #define NF4DQ_CFG_X4_DIRECT 4  /* 16 B/lane packed loads, four strided 16 B stores per lane (no LDS) */
+#define NF4DQ_CFG_A1_AHEAD 8   /* absmax bytes loaded one tile ahead of the packed loads */
 /* bits 8..11: log2 of the number of contiguous tile segments (0..6); block b
  * works in segment b % 2^k (k = 3: one segment per XCD under round-robin placement) */
 #define NF4DQ_CFG_SEG_SHIFT_BIT 8

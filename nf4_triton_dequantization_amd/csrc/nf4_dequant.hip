@@ -136,7 +136,27 @@ struct TileIn {
 
 // Issue the loads of tile `base` (packed bytes) of matrix D.  Buffer loads
 // outside the matrix return 0, so partial tiles need no predicates.
-template <int DT, int MODE, int U, int AUXL, int X4 = 0>
+// Block index (within the whole matrix / stream) of this lane's scale block in tile `base`.
+template <int DT, int U>
+__device__ __forceinline__ uint32_t tile_block(const Desc& D, uint32_t base, uint32_t lane) {
+    constexpr uint32_t kTileBytes = tile_bytes<DT, U>();
+    const uint32_t bsh = D.blk_shift;
+    const uint32_t bpt = kTileBytes >> bsh;  // 0 when one block spans the tile
+    uint32_t g = (base >> bsh) + (bpt ? (lane & (bpt - 1u)) : 0u);
+    const uint32_t nblk = (D.nbytes + (1u << bsh) - 1u) >> bsh;
+    g = g < nblk ? g : nblk - 1u;  // lanes past the end read a valid block; their stores drop
+    return g + D.blk_base;
+}
+
+// Reference mode: the absmax byte of tile `base` on its own, issued a tile ahead of
+// the tile's packed loads (A1A kernels) -- the 1-byte gathers come from a different
+// DRAM row than the packed stream and, issued with it, are the tile's last arrival.
+template <int DT, int U>
+__device__ __forceinline__ uint32_t a1_load(const Desc& D, uint32_t base, uint32_t lane) {
+    return D.a1[fmodu(tile_block<DT, U>(D, base, lane), D.nb)];
+}
+
+template <int DT, int MODE, int U, int AUXL, int X4 = 0, int LOADA1 = 1>
 __device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rsrc_t rp, uint32_t base,
                                                uint32_t lane) {
     constexpr uint32_t LB = lane_bytes<DT>();
@@ -160,15 +180,9 @@ __device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rs
             in.w[j] = __builtin_amdgcn_raw_buffer_load_b16(rp, off, 0, AUXL);
         }
     }
-    constexpr uint32_t kTileBytes = tile_bytes<DT, U>();
-    const uint32_t bsh = D.blk_shift;
-    const uint32_t bpt = kTileBytes >> bsh;  // 0 when one block spans the tile
-    uint32_t g = (base >> bsh) + (bpt ? (lane & (bpt - 1u)) : 0u);
-    const uint32_t nblk = (D.nbytes + (1u << bsh) - 1u) >> bsh;
-    g = g < nblk ? g : nblk - 1u;  // lanes past the end read a valid block; their stores drop
-    g += D.blk_base;               // block index within the whole matrix / stream
+    const uint32_t g = tile_block<DT, U>(D, base, lane);
     if constexpr (MODE == kRef) {
-        in.a1 = D.a1[fmodu(g, D.nb)];
+        if constexpr (LOADA1) in.a1 = D.a1[fmodu(g, D.nb)];
         const uint32_t r = fdiv(g, D.bpr);
         const uint32_t b = g - r * D.bpr.d;
         in.a2 = D.a2[fmodu(r * D.groups + (b >> 2), D.n2)];
@@ -292,8 +306,9 @@ __device__ __forceinline__ void make_rsrcs(const Batch<MAXB>& bt, uint32_t k, __
 // register sets (A, B) so that tile i+1's loads are in flight while tile i is
 // decoded and stored, with no register copies (a copy would force a wait on
 // the loads it copies).
-template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB, int X4 = 0>
+template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB, int X4 = 0, int A1A = 0>
 __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt) {
+    static_assert(!A1A || MODE == kRef, "absmax bytes ahead: reference semantics");
     __shared__ __attribute__((aligned(16))) float lut[16];
     __shared__ __attribute__((aligned(16))) float code2s[MODE == kBnb ? 256 : 1];  // bitsandbytes code (every piece's)
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[X4 ? WPG * 256 : 1];
@@ -317,6 +332,11 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
     __amdgpu_buffer_rsrc_t rpa, roa;
     make_rsrcs<DT>(bt, ca.k, rpa, roa);
     TileIn<U> A = tile_load<DT, MODE, U, AUXL, X4>(bt.d[ca.k], rpa, ca.base, lane);
+    uint32_t a1n = 0;  // A1A: absmax bytes of the wave's next tile
+    if constexpr (A1A) {
+        const Cursor c1 = cursor_at<DT, U>(bt, sm, i0 + nwaves, ca.k);
+        a1n = a1_load<DT, U>(bt.d[c1.k], c1.base, lane);
+    }
     // Out-of-range (dropped) stores with the loop body's count: loop entry then
     // looks like the back edge to hipcc's waitcnt pass ([loads][stores]), so the
     // in-loop waits count past the previous tile's stores instead of draining them.
@@ -342,7 +362,13 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
         const Cursor cb = cursor_at<DT, U>(bt, sm, ca.i + nwaves, ca.k);
         __amdgpu_buffer_rsrc_t rpb = rpa, rob = roa;
         if (MAXB > 1 && cb.k != ca.k) make_rsrcs<DT>(bt, cb.k, rpb, rob);
-        const TileIn<U> B = tile_load<DT, MODE, U, AUXL, X4>(bt.d[cb.k], rpb, cb.base, lane);
+        TileIn<U> B = tile_load<DT, MODE, U, AUXL, X4, !A1A>(bt.d[cb.k], rpb, cb.base, lane);
+        const Cursor cn = cursor_at<DT, U>(bt, sm, cb.i + nwaves, cb.k);
+        uint32_t a1m = 0;
+        if constexpr (A1A) {
+            B.a1 = a1n;
+            a1m = a1_load<DT, U>(bt.d[cn.k], cn.base, lane);
+        }
         tile_finish<DT, MODE, U, AUXS, X4>(bt.d[ca.k], roa, lut, A, ca.base, lane, stage, code2s);
 #if NF4_FLAT_STAMPS
         if (tiles_done == 0) NF4_FSTAMP(1, NF4_FNOW());
@@ -350,10 +376,14 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
 #endif
         if (!cb.valid) break;
 
-        const Cursor cn = cursor_at<DT, U>(bt, sm, cb.i + nwaves, cb.k);
         __amdgpu_buffer_rsrc_t rpn = rpb, ron = rob;
         if (MAXB > 1 && cn.k != cb.k) make_rsrcs<DT>(bt, cn.k, rpn, ron);
-        A = tile_load<DT, MODE, U, AUXL, X4>(bt.d[cn.k], rpn, cn.base, lane);
+        A = tile_load<DT, MODE, U, AUXL, X4, !A1A>(bt.d[cn.k], rpn, cn.base, lane);
+        if constexpr (A1A) {
+            A.a1 = a1m;
+            const Cursor c2 = cursor_at<DT, U>(bt, sm, cn.i + nwaves, cn.k);
+            a1n = a1_load<DT, U>(bt.d[c2.k], c2.base, lane);
+        }
         tile_finish<DT, MODE, U, AUXS, X4>(bt.d[cb.k], rob, lut, B, cb.base, lane, stage, code2s);
 #if NF4_FLAT_STAMPS
         ++tiles_done;
@@ -466,9 +496,9 @@ int cu_count() {
 // of (dtype, U); callers only fill the per-matrix descriptors.  The default
 // configuration instantiates for every dtype and scale mode; the tuning knobs
 // (U = 8, nt loads, workgroup size) exist for reference semantics in fp16/bf16.
-template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB, int X4 = 0>
+template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB, int X4 = 0, int A1A = 0>
 void launch_one(const Batch<MAXB>& b, uint64_t blocks, hipStream_t st) {
-    hipLaunchKernelGGL((nf4_flat_kernel<DT, MODE, U, AUXS, AUXL, WPG, MAXB, X4>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((nf4_flat_kernel<DT, MODE, U, AUXS, AUXL, WPG, MAXB, X4, A1A>), dim3((unsigned)blocks),
                        dim3(64 * WPG), 0, st, b);
 }
 
@@ -538,6 +568,15 @@ int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_laun
     const uint32_t pol = (uint32_t)((cfg.flags >> NF4DQ_CFG_STORE_POLICY_BIT) & 0xF);
     if ((cfg.flags & (NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_X4_LOADS)) && (mode != kRef || dtype == NF4DQ_F32))
         return NF4DQ_ERR_ARG;  // the 16 B/lane shapes: reference semantics, 16-bit outputs
+    if (cfg.flags & NF4DQ_CFG_A1_AHEAD) {  // absmax bytes a tile ahead: base shape, reference semantics
+        if (U != 4 || wpg != 4 || !cfg.nontemporal || pol || ntl || mode != kRef ||
+            (cfg.flags & (NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT)))
+            return NF4DQ_ERR_ARG;
+        if (dtype == NF4DQ_BF16) launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, 0, 4, MAXB, 0, 1>(b, blocks, st);
+        else if (dtype == NF4DQ_F16) launch_one<NF4DQ_F16, kRef, 4, kAuxStore, 0, 4, MAXB, 0, 1>(b, blocks, st);
+        else launch_one<NF4DQ_F32, kRef, 4, kAuxStore, 0, 4, MAXB, 0, 1>(b, blocks, st);
+        return hip_rc(hipGetLastError());
+    }
     if (cfg.flags & NF4DQ_CFG_X4_DIRECT) {  // 16 B/lane loads, strided 16 B stores: base shape only
         if (U != 4 || wpg != 4 || !cfg.nontemporal || pol || (cfg.flags & NF4DQ_CFG_X4_LOADS)) return NF4DQ_ERR_ARG;
         if (dtype == NF4DQ_BF16) {
@@ -745,15 +784,17 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len, const uint8_t
                         const nf4_launch_cfg* cfg, void* hip_stream) {
     nf4_launch_cfg c = cfg ? *cfg : kDefaultCfg;
     if (c.tile_dwords != 1 && c.tile_dwords != 2 && c.tile_dwords != 4 && c.tile_dwords != 8) return NF4DQ_ERR_ARG;
-    if (c.tile_dwords < 4 && (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_STORE_POLICY_MASK)))
+    if (c.tile_dwords < 4 && (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_A1_AHEAD |
+                                NF4DQ_CFG_STORE_POLICY_MASK)))
         return NF4DQ_ERR_ARG;
-    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_SEG_SHIFT_MASK | NF4DQ_CFG_WG_SHIFT_MASK |
+    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_A1_AHEAD | NF4DQ_CFG_SEG_SHIFT_MASK | NF4DQ_CFG_WG_SHIFT_MASK |
                     NF4DQ_CFG_STORE_POLICY_MASK))
         return NF4DQ_ERR_ARG;
     if (((c.flags >> NF4DQ_CFG_SEG_SHIFT_BIT) & 0xF) > 6) return NF4DQ_ERR_ARG;
     if (((c.flags >> NF4DQ_CFG_WG_SHIFT_BIT) & 0xF) > 4) return NF4DQ_ERR_ARG;
     if (((c.flags >> NF4DQ_CFG_STORE_POLICY_BIT) & 0xF) > 5) return NF4DQ_ERR_ARG;
-    if (!c.nontemporal && (c.tile_dwords != 4 || (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_WG_SHIFT_MASK))))
+    if (!c.nontemporal && (c.tile_dwords != 4 || (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_WG_SHIFT_MASK |
+                                                             NF4DQ_CFG_A1_AHEAD | NF4DQ_CFG_X4_DIRECT))))
         return NF4DQ_ERR_ARG;
     return ref_impl(packed, packed_len, absmax_q, nb, absmax2, n2, out, out_dtype, m, n, c,
                     reinterpret_cast<hipStream_t>(hip_stream));
