@@ -2,8 +2,8 @@
 
 Compares, in one process (interleaved rounds), 4096^2 and 8192^2 NF4->bf16 over
 rotating packed/output buffers with (a) one shared absmax/nested-absmax pair and
-(b) a separate pair per buffer set (what bench.py does), plus the output-value
-sensitivity check (a2 = rand / tiny / 1 / 0).
+(b) a separate pair per buffer set (what bench.py does), (c) per-set absmax bytes
+as slices of one large allocation.
 """
 import ctypes, json, os, sys  # noqa: E401
 
@@ -23,9 +23,18 @@ for (m, n, P) in ((4096, 4096, 16), (8192, 8192, 8)):
     outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(P)]
     a1s = [torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev) for _ in range(P)]
     a2s = [torch.rand(n2, device=dev) * 0.01 + 1e-3 for _ in range(P)]
+    # the same per-set bytes as views into one large allocation (2 MiB-aligned slices):
+    # separates "different bytes per set" from "separate small-pool allocations"
+    slab = torch.empty(P * (2 << 20), dtype=torch.uint8, device=dev)
+    a1v = [slab[i * (2 << 20): i * (2 << 20) + nb] for i in range(P)]
+    for i in range(P):
+        a1v[i].copy_(a1s[i])
+    print(json.dumps({"m": m, "a1_alloc": [int(t.data_ptr()) % (2 << 20) for t in a1s[:4]],
+                      "slab_mod_2MiB": int(slab.data_ptr()) % (2 << 20)}), flush=True)
     variants = {"shared a1/a2": lambda i: (a1s[0], a2s[0]), "per-set a1/a2": lambda i: (a1s[i % P], a2s[i % P]),
                 "per-set a1, shared a2": lambda i: (a1s[i % P], a2s[0]),
-                "shared a1, per-set a2": lambda i: (a1s[0], a2s[i % P])}
+                "shared a1, per-set a2": lambda i: (a1s[0], a2s[i % P]),
+                "per-set a1 in one slab, shared a2": lambda i: (a1v[i % P], a2s[0])}
     for r in range(3):
         for name, pick in variants.items():
             def deq(i, pick=pick):
