@@ -113,6 +113,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])
+    ap.add_argument("--no-c5", action="store_true", help="skip the BASELINE configs[4] section of the result line")
+    ap.add_argument("--c5-shape", default="8192x8192", type=lambda v: tuple(int(x) for x in v.split("x")),
+                    help="matrix shape of the c5 section (CPU rehearsals use a small one)")
     ap.add_argument("--dist-backend", default=None, help="nccl (= RCCL, default on GPUs) or gloo (rehearsal)")
     return ap.parse_args(argv)
 
@@ -158,9 +161,26 @@ def spawn_ranks(n: int) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    # poll every rank: the first one to fail ends the others (they would otherwise sit
+    # in init_process_group or a barrier until the backend's timeout)
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            log(f"bench.py: a rank exited with {bad[0]}; the other ranks were stopped")
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.05)
 
 
 # ---------------------------------------------------------------------------
@@ -258,197 +278,136 @@ def find_traffic(m, n, dtype):
     return None, None
 
 
-def main():
-    args = parse_args()
-    if args.lead == "auto":
-        args.lead = "none" if args.launch == "graph" and not args.no_graph else "spin-steps"
-    world_env = os.environ.get("WORLD_SIZE")
-    if world_env is None and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus))
-    world = int(world_env or "1")
-    if world != args.gpus:
-        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; they must agree")
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # stdout carries exactly one line, the result: anything the runtime libraries
-    # print there (gloo's connection notes, RCCL / HIP warnings) goes to stderr
-    result_out = os.fdopen(os.dup(1), "w")
-    sys.stdout.flush()
-    os.dup2(2, 1)
+class Workload:
+    """One rank's share of a workload: its matrices, P rotating buffer sets of them on
+    the device (packed weight, this rank's scattered quant statistics, output), and
+    one bound C-ABI call per set (arguments prepared up front)."""
 
+    def __init__(self, args, mats, stats, dev, dt, code, cfg_p, cpu):
+        import torch
+
+        import workloads as W
+        from nf4_triton_dequantization_amd import _lib
+
+        self.mats, self.cpu, self.code = mats, cpu, code
+        self.L = _lib.lib()
+        step_bytes = sum(m * n // 2 + 2 * m * n for _, m, n in mats)  # packed + output per step
+        P = args.sets or max(2, -(-MIN_FOOTPRINT // max(1, step_bytes)))
+        if cpu:
+            P = args.sets or 2
+        elif not args.sets:
+            # across the untimed -> timed boundary set 0 is reused after
+            # K - P*floor((K-1)/P) steps (K when P >= K): keep that >= 256 MiB so no set
+            # is still in the Infinity Cache when a timed step reaches it
+            def reuse(p):
+                return args.steps if p >= args.steps else args.steps - p * ((args.steps - 1) // p)
+
+            while P < args.steps and reuse(P) * step_bytes < (256 << 20):
+                P += 1
+        self.P = P
+        # one host generation per matrix; the P sets are device copies (distinct
+        # addresses are what keep a set out of the caches, not distinct contents)
+        base = []
+        for (gid, m, n), st in zip(mats, stats):
+            q = torch.from_numpy(W.splitmix64_bytes(3409 + 7919 * gid, m * n // 2, stream=1)).to(dev)
+            base.append((q, st.absmax.to(dev), st.absmax2.to(dev), m, n))
+        self.sets = []
+        for s in range(P):
+            row = []
+            for (q, a1, a2, m, n) in base:
+                if s:
+                    q, a1, a2 = q.clone(), a1.clone(), a2.clone()
+                row.append((q, a1, a2, torch.empty((m, n), dtype=dt, device=dev), m, n))
+            self.sets.append(row)
+        self.descs = [(_lib.MatrixDesc * len(row))(*[
+            _lib.MatrixDesc(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                            out.data_ptr(), m, n) for (q, a1, a2, out, m, n) in row]) for row in self.sets]
+        self.fast = []
+        if not cpu:
+            sp = torch.cuda.current_stream(dev).cuda_stream
+            default_cfg = cfg_p is None
+            for s_i, row in enumerate(self.sets):
+                if len(row) == 1:
+                    q, a1, a2, out, m, n = row[0]
+                    a = (q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                         out.data_ptr(), code, m, n)
+                    fn = self.L.nf4_dequant_ref if default_cfg else self.L.nf4_dequant_ref_cfg
+                    a = a + ((sp,) if default_cfg else (cfg_p, sp))
+                else:
+                    fn, a = self.L.nf4_dequant_ref_batched, (self.descs[s_i], len(row), code, sp)
+
+                def call(fn=fn, a=a):
+                    rc = fn(*a)
+                    if rc:
+                        raise RuntimeError(f"nf4 dequant launch: {_lib.strerror(rc)}")
+                self.fast.append(call)
+
+    def launch(self, i):
+        if not self.cpu:
+            self.fast[i % self.P]()
+            return
+        from nf4_triton_dequantization_amd import _lib
+
+        for (q, a1, a2, out, m, n) in self.sets[i % self.P]:
+            rc = self.L.nf4_dequant_ref_cpu(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(),
+                                            a2.numel(), out.data_ptr(), self.code, m, n, 0)
+            if rc:
+                raise RuntimeError(f"nf4_dequant_ref_cpu: {_lib.strerror(rc)}")
+
+    def sanity(self, dtype_name):
+        """Set 0 against the oracle on the first 64 rows of each matrix (the checker;
+        tests/ do the full job)."""
+        import torch
+
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import nf4_oracle as O
+
+        for (q, a1, a2, out, m, n) in self.sets[0]:
+            r = min(64, m)
+            want = O.dequant_ref_np(q[: r * n // 2].cpu().numpy(), a1.cpu().numpy(), a2.cpu().numpy(), r, n,
+                                    O.BF16 if dtype_name == "bf16" else O.F16)
+            got = out[:r].contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+            if not np.array_equal(got, want):
+                raise RuntimeError("bench sanity check failed: output differs from the oracle")
+        return True
+
+    def elements(self):
+        return sum(m * n for _, m, n in self.mats)
+
+    def alg_bytes(self):
+        return sum(algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256) for _, m, n in self.mats)
+
+
+def time_steps(args, wl, dev, world, graph_ok=True):
+    """Warmup, one untimed pass over every buffer set, then the timed region (see the
+    module docstring); returns (ms for K steps on this rank, launch mode)."""
     import torch
     import torch.distributed as dist
 
-    from nf4_triton_dequantization_amd import _lib
-    from nf4_triton_dequantization_amd.sharding import QuantStats, broadcast_quant_stats, max_over_ranks
-    import workloads as W
-
-    cpu = args.backend == "cpu"
-    dist_backend = args.dist_backend or ("gloo" if cpu else "nccl")
-    if cpu:
-        dev = torch.device("cpu")
-    else:
-        # rehearsal with more ranks than GPUs (gloo only): ranks share devices
-        ndev = torch.cuda.device_count()
-        local_dev = local if dist_backend == "nccl" else local % max(1, ndev)
-        torch.cuda.set_device(local_dev)
-        dev = torch.device("cuda", local_dev)
-    if world > 1:
-        if dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(dist_backend)
-
-    mats = rank_matrices(args, rank, world)
-    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
-    code = _lib.BF16 if args.dtype == "bf16" else _lib.F16
-    L = _lib.lib()
-
-    def sync():
-        if not cpu:
-            torch.cuda.synchronize()
-
-    # ---- setup: quant stats of every rank's matrices on rank 0, broadcast once ----
-    step_bytes = sum(m * n // 2 + 2 * m * n for _, m, n in mats)  # packed + output per step (this rank)
-    P = args.sets or max(2, -(-MIN_FOOTPRINT // max(1, step_bytes)))
-    if cpu:
-        P = args.sets or 2
-    elif not args.sets:
-        # across the boundary between two replays set 0 is reused after
-        # K - P*floor((K-1)/P) steps (K when P >= K): keep that >= 256 MiB so no set
-        # is still in the Infinity Cache when the timed replay reaches it
-        def reuse(p):
-            return args.steps if p >= args.steps else args.steps - p * ((args.steps - 1) // p)
-
-        while P < args.steps and reuse(P) * step_bytes < (256 << 20):
-            P += 1
-    all_mats = [rank_matrices(args, r, world) for r in range(world)]
-    t_setup = time.perf_counter()
-    if rank == 0:
-        stats = []
-        for r in range(world):
-            for s in range(P):
-                for gid, m, n in all_mats[r]:
-                    seed = 3409 + 7919 * gid + 104729 * s
-                    nb = m * n // 64
-                    stats.append(QuantStats(m, n, torch.from_numpy(W.splitmix64_bytes(seed, nb, stream=2)),
-                                            torch.from_numpy(W.uniform_f32(seed, (nb + 255) // 256, 1e-3, 1e-2,
-                                                                           stream=3)), dt))
-    else:
-        stats = None
-    if world > 1:
-        sync()
-        tb = time.perf_counter()
-        stats = broadcast_quant_stats(stats, dev, src=0)
-        sync()
-        bcast_ms = (time.perf_counter() - tb) * 1e3
-    else:
-        stats = [QuantStats(s.m, s.n, s.absmax.to(dev), s.absmax2.to(dev), s.dtype) for s in stats]
-        bcast_ms = 0.0
-    per_rank = P * len(mats)
-    mine = stats[rank * per_rank:(rank + 1) * per_rank]
-    sets = []  # sets[s] = [(q, a1, a2, out, m, n)] for this rank's matrices
-    k = 0
-    for s in range(P):
-        row = []
-        for gid, m, n in mats:
-            seed = 3409 + 7919 * gid + 104729 * s
-            q = torch.from_numpy(W.splitmix64_bytes(seed, m * n // 2, stream=1)).to(dev)
-            out = torch.empty((m, n), dtype=dt, device=dev)
-            row.append((q, mine[k].absmax, mine[k].absmax2, out, m, n))
-            k += 1
-        sets.append(row)
-    sync()
-    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s, {P} buffer sets x {len(mats)} matrices, "
-        f"quant_state broadcast {bcast_ms:.2f} ms")
-
-    cfg = _lib.LaunchCfg(args.tile_dwords, args.blocks_per_cu, args.nontemporal, args.flags)
-    cfg_p = ctypes.byref(cfg)
-    descs = []
-    for row in sets:
-        arr = (_lib.MatrixDesc * len(row))(*[
-            _lib.MatrixDesc(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
-                            out.data_ptr(), m, n) for (q, a1, a2, out, m, n) in row])
-        descs.append(arr)
-
-    def launch(i):
-        row = sets[i % P]
-        if cpu:
-            for (q, a1, a2, out, m, n) in row:
-                rc = L.nf4_dequant_ref_cpu(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(),
-                                           a2.numel(), out.data_ptr(), code, m, n, 0)
-                if rc:
-                    raise RuntimeError(f"nf4_dequant_ref_cpu: {_lib.strerror(rc)}")
-            return
-        sp = torch.cuda.current_stream(dev).cuda_stream
-        if len(row) == 1:
-            q, a1, a2, out, m, n = row[0]
-            rc = L.nf4_dequant_ref_cfg(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(),
-                                       a2.numel(), out.data_ptr(), code, m, n, cfg_p, sp)
-        else:
-            rc = L.nf4_dequant_ref_batched(descs[i % P], len(row), code, sp)
-        if rc:
-            raise RuntimeError(f"nf4 dequant launch: {_lib.strerror(rc)}")
-
-    # eager timed loop: one bound C-ABI call per step, arguments prepared up front
-    # (the product entry nf4_dequant_ref when the launch configuration is the default)
-    fast = []
-    if not cpu:
-        sp0 = torch.cuda.current_stream(dev).cuda_stream
-        default_cfg = (args.tile_dwords, args.blocks_per_cu, args.nontemporal, args.flags) == (4, 0, 1, 0)
-        for s_i, row in enumerate(sets):
-            if len(row) == 1:
-                q, a1, a2, out, m, n = row[0]
-                a = (q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(), out.data_ptr(),
-                     code, m, n)
-                fn = L.nf4_dequant_ref if default_cfg else L.nf4_dequant_ref_cfg
-                a = a + ((sp0,) if default_cfg else (cfg_p, sp0))
-            else:
-                fn, a = L.nf4_dequant_ref_batched, (descs[s_i], len(row), code, sp0)
-
-            def call(fn=fn, a=a):
-                rc = fn(*a)
-                if rc:
-                    raise RuntimeError(f"nf4 dequant launch: {_lib.strerror(rc)}")
-            fast.append(call)
+    cpu = wl.cpu
+    P = wl.P
     lead_n = min(args.lead_n, P)
-
-    # correctness sanity of set 0 against the oracle on the first 64 rows of each
-    # matrix (the checker; tests/ do the full job)
-    launch(0)
-    sync()
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import nf4_oracle as O
-
-    for (q, a1, a2, out, m, n) in sets[0]:
-        want = O.dequant_ref_np(q[: 64 * n // 2].cpu().numpy(), a1.cpu().numpy(), a2.cpu().numpy(), 64, n,
-                                O.BF16 if args.dtype == "bf16" else O.F16)
-        got = out[:64].contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
-        if not np.array_equal(got, want):
-            raise RuntimeError("bench sanity check failed: output differs from the oracle")
-
-    # ---- warmup + graph capture ------------------------------------------------------
     for w in range(args.warmup):
-        launch(w)
+        wl.launch(w)
     if not cpu:
         # one untimed pass over every buffer set: the first touch of a set's pages
         # costs +1.5-3 us per 42 MB launch in GPU TLB misses (profiles/r02/bench_lead_ab.txt,
         # profiles/r02/bench_eager_ab.txt) -- the steady state of a resident weight
         # set is TLB-warm; the graph path's untimed replay did this implicitly
         for s_i in range(P):
-            fast[s_i]()
-    sync()
+            wl.fast[s_i]()
+        torch.cuda.synchronize()
     graph = None
-    if not cpu and args.launch == "graph" and not args.no_graph:
+    if graph_ok and not cpu and args.launch == "graph" and not args.no_graph:
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 for i in range(args.steps):
-                    launch(i)
+                    wl.launch(i)
             graph.replay()  # upload + one untimed pass
             torch.cuda.synchronize()
         except Exception as e:  # capture unsupported -> eager issue, reported in config
-            log(f"[rank {rank}] hipGraph capture failed ({e}); timing eager launches")
+            log(f"hipGraph capture failed ({e}); timing eager launches")
             graph = None
             torch.cuda.synchronize()
     if not cpu and args.flush:
@@ -459,22 +418,22 @@ def main():
         scratch.fill_(1)
         torch.cuda.synchronize()
         del scratch
-
-    # ---- timed region --------------------------------------------------------------------
     if not cpu and args.lead == "spin-steps":
         _spin_rate_calibrate()
     if world > 1:
         dist.barrier()
-    sync()
+    if not cpu:
+        torch.cuda.synchronize()
     if cpu:
         t0 = time.perf_counter()
         for i in range(args.steps):
-            launch(i)
+            wl.launch(i)
         t_ms = (time.perf_counter() - t0) * 1e3
     else:
         main_stream = torch.cuda.current_stream(dev)
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
+        fast = wl.fast
         if graph is not None and args.lead == "replay":
             # one more untimed replay enqueued right ahead of the start event: the
             # timed steps follow warm steps back to back (as in a steady stream of
@@ -507,17 +466,220 @@ def main():
         t_ms = ev0.elapsed_time(ev1)
     if world > 1:
         dist.barrier()
-    my_ms = t_ms
-    per_rank_ms = [my_ms]
+    mode = "hipGraph" if graph is not None else ("host loop" if cpu else "eager")
+    return t_ms, mode
+
+
+def gather_times(my_ms, dev, world):
+    """(max over ranks, every rank's figure)."""
+    if world == 1:
+        return my_ms, [my_ms]
+    import torch.distributed as dist
+
+    from nf4_triton_dequantization_amd.sharding import max_over_ranks
+
+    t = max_over_ranks(my_ms, dev)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, my_ms)
+    return t, gathered
+
+
+def distribute_stats(all_mats, rank, world, dev, dt, cpu):
+    """Rank 0 holds every matrix's quant statistics (as after loading a checkpoint);
+    each rank receives only its own matrices' (sharding.scatter_quant_stats over
+    RCCL).  Returns (this rank's stats, ms the distribution took)."""
+    import torch
+
+    import workloads as W
+    from nf4_triton_dequantization_amd.sharding import QuantStats, scatter_quant_stats
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
+    per_rank = None
+    if rank == 0:
+        per_rank = []
+        for r in range(world):
+            row = []
+            for gid, m, n in all_mats[r]:
+                seed = 3409 + 7919 * gid
+                nb = m * n // 64
+                row.append(QuantStats(m, n, torch.from_numpy(W.splitmix64_bytes(seed, nb, stream=2)),
+                                      torch.from_numpy(W.uniform_f32(seed, (nb + 255) // 256, 1e-3, 1e-2,
+                                                                     stream=3)), dt))
+            per_rank.append(row)
+    if world == 1:
+        return [QuantStats(s.m, s.n, s.absmax.to(dev), s.absmax2.to(dev), s.dtype) for s in per_rank[0]], 0.0
+    import torch.distributed as dist
+
+    dist.barrier()
+    sync()
+    tb = time.perf_counter()
+    mine = scatter_quant_stats(per_rank, dev, src=0)
+    sync()
+    return mine, (time.perf_counter() - tb) * 1e3
+
+
+def rank_figures(all_mats, per_rank_ms, steps):
+    out = []
+    for r, ms in enumerate(per_rank_ms):
+        el = sum(m * n for _, m, n in all_mats[r])
+        by = sum(algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256) for _, m, n in all_mats[r])
+        out.append({"rank": r, "matrices": len(all_mats[r]), "ms_per_step": ms / steps,
+                    "elements_per_s": el * steps / (ms * 1e-3), "GBps": by * steps / (ms * 1e-3) / 1e9})
+    return out
+
+
+def c5_section(args, rank, world, dev, dt, code, cpu):
+    """BASELINE configs[4] at this N: the 8 independent c5 matrices split round-robin
+    over the ranks (one per GPU at N = 8), each rank's share one launch per step
+    (the single-matrix entry at N = 8, the batched one below), quant statistics
+    scattered from rank 0.  Aggregate = 8 matrices / the slowest rank's time."""
+    import torch
+
+    import workloads as W
+
+    m, n = args.c5_shape
+    all_mats = [[(g, m, n) for g in range(r, W.C5_MATRICES, world)] for r in range(world)]
+    mats = all_mats[rank]
+    stats, scatter_ms = distribute_stats(all_mats, rank, world, dev, dt, cpu)
+    wl = Workload(args, mats, stats, dev, dt, code, None, cpu)
+    wl.launch(0)
+    if not cpu:
+        torch.cuda.synchronize()
+    verified = wl.sanity(args.dtype) if mats else True
+    my_ms, _mode = time_steps(args, wl, dev, world, graph_ok=False)
+    t_ms, per = gather_times(my_ms, dev, world)
+    els = W.C5_MATRICES * m * n
+    alg = W.C5_MATRICES * algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256)
+    per_rank = rank_figures(all_mats, per, args.steps)
+    gbps = alg * args.steps / (t_ms * 1e-3) / 1e9
+    res = {
+        "config": f"c5: {W.C5_MATRICES} independent {m}x{n} NF4->{args.dtype} matrices (BASELINE configs[4]) "
+                  f"split round-robin over {world} rank(s)",
+        "matrices": W.C5_MATRICES, "shape": [m, n], "n_gpus": world, "steps": args.steps,
+        "ms_per_step": t_ms / args.steps, "elements_per_s": els * args.steps / (t_ms * 1e-3), "GBps": gbps,
+        "frac_of_peak": None if cpu else gbps * 1e9 / (PEAK_HBM * world),
+        "per_rank": per_rank, "scaling": "strong",
+        "launch": ("one nf4_dequant_ref launch per rank per step" if max(len(a) for a in all_mats) == 1 else
+                   "each rank's share in one nf4_dequant_ref_batched launch per step"),
+        "buffer_sets": wl.P, "quant_state_scatter_ms": round(scatter_ms, 3),
+        "quant_state_bytes_per_rank": [sum(m * n // 64 + 4 * ((m * n // 64 + 255) // 256) for _ in a)
+                                       for a in all_mats],
+        "verified_first_rows": bool(verified),
+    }
+    del wl
+    if not cpu:
+        torch.cuda.empty_cache()
+    return res
+
+
+def c5_cpu_figures(args, code, threads):
+    """Host-CPU figures for one c5 matrix on rank 0: this library's host path (native)
+    and the reference-structure torch port, one matrix each (bounded sample)."""
+    import torch
+
+    import workloads as W
+    from nf4_triton_dequantization_amd import _lib
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import fallback_torch as F
+
+    m, n = args.c5_shape
+    p, a1, a2 = W.make_inputs(m, n, 3409)
+    out = np.empty((m, n), np.uint16)
+    L = _lib.lib()
+    t0 = time.perf_counter()
+    reps = 0
+    while reps < 3 or time.perf_counter() - t0 < 1.0:
+        rc = L.nf4_dequant_ref_cpu(p.ctypes.data, p.size, a1.ctypes.data, a1.size, a2.ctypes.data, a2.size,
+                                   out.ctypes.data, code, m, n, threads)
+        if rc:
+            raise RuntimeError(f"nf4_dequant_ref_cpu: {_lib.strerror(rc)}")
+        reps += 1
+    native = reps * m * n / (time.perf_counter() - t0)
+    tdt = torch.bfloat16 if code == _lib.BF16 else torch.float16
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        t0 = time.perf_counter()
+        F.dequant_fallback(torch.from_numpy(p), torch.from_numpy(a1), torch.from_numpy(a2), m, n, tdt)
+        port = m * n / (time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev)
+    return {"unit": "elements/s", "cores": threads, "kind": "port", "value": port, "native": native,
+            "sample": f"one {m}x{n} matrix: oracle/fallback_torch.py once, nf4_dequant_ref_cpu x{reps}"}
+
+
+def main():
+    args = parse_args()
+    if args.lead == "auto":
+        args.lead = "none" if args.launch == "graph" and not args.no_graph else "spin-steps"
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; they must agree")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("NF4_BENCH_FAIL_RANK") == str(rank):  # test hook: a rank that dies at startup
+        raise SystemExit(f"bench.py: rank {rank} failing on request (NF4_BENCH_FAIL_RANK)")
+    # stdout carries exactly one line, the result: anything the runtime libraries
+    # print there (gloo's connection notes, RCCL / HIP warnings) goes to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
+    import torch
+    import torch.distributed as dist
+
+    from nf4_triton_dequantization_amd import _lib
+
+    cpu = args.backend == "cpu"
+    dist_backend = args.dist_backend or ("gloo" if cpu else "nccl")
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        # rehearsal with more ranks than GPUs (gloo only): ranks share devices
+        ndev = torch.cuda.device_count()
+        local_dev = local if dist_backend == "nccl" else local % max(1, ndev)
+        torch.cuda.set_device(local_dev)
+        dev = torch.device("cuda", local_dev)
     if world > 1:
-        t_ms = max_over_ranks(my_ms, dev)
-        gathered = [None] * world
-        dist.all_gather_object(gathered, my_ms)
-        per_rank_ms = gathered
+        if dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(dist_backend)
+
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
+    code = _lib.BF16 if args.dtype == "bf16" else _lib.F16
+    cfg = _lib.LaunchCfg(args.tile_dwords, args.blocks_per_cu, args.nontemporal, args.flags)
+    default_cfg = (args.tile_dwords, args.blocks_per_cu, args.nontemporal, args.flags) == (4, 0, 1, 0)
+    cfg_p = None if default_cfg else ctypes.byref(cfg)
+
+    # ---- headline workload: setup (quant statistics scattered from rank 0) ----------------
+    all_mats = [rank_matrices(args, r, world) for r in range(world)]
+    mats = all_mats[rank]
+    t_setup = time.perf_counter()
+    stats, scatter_ms = distribute_stats(all_mats, rank, world, dev, dt, cpu)
+    wl = Workload(args, mats, stats, dev, dt, code, cfg_p, cpu)
+    if not cpu:
+        torch.cuda.synchronize()
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s, {wl.P} buffer sets x {len(mats)} matrices, "
+        f"quant_state scatter {scatter_ms:.2f} ms")
+    wl.launch(0)
+    if not cpu:
+        torch.cuda.synchronize()
+    wl.sanity(args.dtype)
+
+    # ---- timed region -------------------------------------------------------------------------
+    my_ms, launch_mode = time_steps(args, wl, dev, world)
+    t_ms, per_rank_ms = gather_times(my_ms, dev, world)
 
     # ---- figures -------------------------------------------------------------------------------
-    my_elems = sum(m * n for _, m, n in mats)
-    my_alg = sum(algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256) for _, m, n in mats)
+    my_alg = wl.alg_bytes()
     launches_per_step = 1 if not cpu else len(mats)
     all_elems = sum(m * n for r in range(world) for _, m, n in all_mats[r])
     all_alg = sum(algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256)
@@ -529,6 +691,9 @@ def main():
     if not cpu and len(mats) == 1:
         traffic, traffic_src = find_traffic(m0, n0, args.dtype)
     achieved = my_alg / launches_per_step / (kt_mean * 1e-6)
+    del wl
+    if not cpu:
+        torch.cuda.empty_cache()
     if args.workload == "c5":
         metric = "dequantized elements/s (8 x 8192x8192 NF4->bf16, one matrix per GPU at N=8)"
         workload = (f"c5: 8 independent 8192x8192 NF4->{args.dtype} matrices (BASELINE configs[4]) split "
@@ -553,20 +718,16 @@ def main():
         "dtype": "f32",
         "data": "synthetic (splitmix64 packed weights + absmax, resident in HBM)",
         "hbm_gb_s": all_alg * args.steps / (t_ms * 1e-3) / 1e9,
-        "per_rank": [{"rank": r, "ms_per_step": per_rank_ms[r] / args.steps,
-                      "elements_per_s": sum(m * n for _, m, n in all_mats[r]) * args.steps / (per_rank_ms[r] * 1e-3),
-                      "GBps": sum(algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256)
-                                  for _, m, n in all_mats[r]) * args.steps / (per_rank_ms[r] * 1e-3) / 1e9}
-                     for r in range(world)],
+        "per_rank": rank_figures(all_mats, per_rank_ms, args.steps),
         "config": {
             "workload": workload,
             "matrices_per_rank": len(mats), "m": m0, "n": n0, "out_dtype": args.dtype,
             "arith": "u8 unpack, fp32 scale/multiply, RNE to bf16/fp16", "backend": args.backend,
-            "buffer_sets": P, "launch": "hipGraph" if graph is not None else ("host loop" if cpu else "eager"),
+            "buffer_sets": args.sets or None, "launch": launch_mode,
             "tile_dwords": args.tile_dwords, "blocks_per_cu": args.blocks_per_cu, "nontemporal": args.nontemporal,
             "flags": args.flags, "parallelism": f"shard{world} (independent matrices)",
             "cache_flush_before_timing": bool(not cpu and args.flush), "lead": args.lead,
-            "quant_state_broadcast_ms": round(bcast_ms, 3), "dist_backend": dist_backend if world > 1 else None,
+            "quant_state_scatter_ms": round(scatter_ms, 3), "dist_backend": dist_backend if world > 1 else None,
         },
         "roofline": None if cpu else {
             "bound": "hbm",
@@ -582,9 +743,17 @@ def main():
             "algorithmic_bytes_per_launch": my_alg // launches_per_step,
         },
         "cpu_baseline": None,
+        "c5": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cpu:
+    # ---- BASELINE configs[4] at this N (every N: the driver's scaling runs carry it) --------
+    if not args.no_c5 and args.workload != "c5":
+        res["c5"] = c5_section(args, rank, world, dev, dt, code, cpu)
+    # ---- CPU baseline: rank 0, after every timed region, at every N ---------------------------
+    if rank == 0 and not args.no_cpu_baseline:
+        threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
         res["cpu_baseline"] = cpu_baseline(mats, args.cpu_seconds, code)
+        if res["c5"] is not None:
+            res["c5"]["cpu_baseline"] = c5_cpu_figures(args, code, threads)
     if rank == 0:
         print(json.dumps(res), file=result_out, flush=True)
     if world > 1:

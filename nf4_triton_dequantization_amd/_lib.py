@@ -15,7 +15,8 @@ import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NF4DQ_LIB_PATH: load a diagnostic build of the same library instead (tools/Makefile);
-# unset in every product / test / bench run
+# unset in every product / test / bench run (when set, the tensor-level entry is not
+# loaded, so every call goes to that build)
 LIB_PATH = os.environ.get("NF4DQ_LIB_PATH") or os.path.join(_HERE, "_lib", "libnf4dq.so")
 EXT_PATH = os.path.join(_HERE, "_lib", "nf4ext.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nf4_dequant.h")
@@ -142,20 +143,35 @@ _ext_tried = False
 
 
 def ext():
-    """The tensor-level fast entry (``_lib/nf4ext.so``, csrc/nf4_torch_ext.cpp), or None
-    when it is not built: callers then take the ctypes route to the same kernels."""
+    """The tensor-level fast entry (``_lib/nf4ext.so``, csrc/nf4_torch_ext.cpp), or None:
+    callers then take the ctypes route to the same kernels.
+
+    None when the extension is not built, when it fails to load (a stale build or a
+    torch ABI mismatch: a warning names the error), and when ``NF4DQ_LIB_PATH``
+    selects another build of the C ABI -- the extension links the product
+    ``_lib/libnf4dq.so`` through its rpath, so loading it then would put two copies
+    of the library in the process and the drop-in would run the other one.
+    Raises like ``lib()`` when the C ABI itself is missing.
+    """
     global _ext, _ext_tried
     if not _ext_tried:
         lib()  # the C ABI first (the extension links it; one copy per process); takes _lock itself
         with _lock:
             if not _ext_tried:
-                if os.path.exists(EXT_PATH):
+                if os.path.exists(EXT_PATH) and not os.environ.get("NF4DQ_LIB_PATH"):
                     import importlib.util
 
-                    spec = importlib.util.spec_from_file_location("nf4ext", EXT_PATH)
-                    mod = importlib.util.module_from_spec(spec)
-                    spec.loader.exec_module(mod)
-                    _ext = mod
+                    try:
+                        spec = importlib.util.spec_from_file_location("nf4ext", EXT_PATH)
+                        mod = importlib.util.module_from_spec(spec)
+                        spec.loader.exec_module(mod)
+                        _ext = mod
+                    except (ImportError, OSError) as e:
+                        import warnings
+
+                        warnings.warn(f"nf4ext.so did not load ({e}); the drop-in uses the ctypes route "
+                                      f"to the same kernels", RuntimeWarning, stacklevel=2)
+                        _ext = None
                 _ext_tried = True
     return _ext
 

@@ -191,7 +191,18 @@ def _launch_cpu(qweight, absmax, absmax32, out, m, n, code) -> None:
 _REF = None  # bound nf4_dequant_ref (fast path: one attribute lookup less per call)
 _raw_stream = torch._C._cuda_getCurrentRawStream  # device index -> hipStream_t of the current stream
 _U8, _F32 = torch.uint8, torch.float32
-_EXT = _lib.ext()  # tensor-level fast entry (csrc/nf4_torch_ext.cpp), None when not built
+# tensor-level fast entry (csrc/nf4_torch_ext.cpp), resolved on the first drop-in call
+# (importing the package loads no native code; a missing libnf4dq.so raises there)
+_EXT = None
+_EXT_READY = False
+
+
+def _ext():
+    global _EXT, _EXT_READY
+    if not _EXT_READY:
+        _EXT = _lib.ext()  # raises when libnf4dq.so is missing; None when nf4ext.so is absent / unusable
+        _EXT_READY = True
+    return _EXT
 
 
 def _dequantize(qweight, absmax, absmax32, dtype, m, n) -> torch.Tensor:
@@ -200,10 +211,11 @@ def _dequantize(qweight, absmax, absmax32, dtype, m, n) -> torch.Tensor:
         # fp64 output = the fp32 product, widened exactly
         return _dequantize(qweight, absmax, absmax32, torch.float32, m, n).to(torch.float64)
     code = _dtype_code(dtype)  # raise before allocating
-    if _EXT is not None:
+    ext = _EXT if _EXT_READY else _ext()
+    if ext is not None:
         # uint8 / uint8 / fp32 contiguous device tensors: checks, allocation, stream
         # and launch in one C++ call (None = this call needs the general path below)
-        out = _EXT.dequant_ref(qweight, absmax, absmax32, m, n, code)
+        out = ext.dequant_ref(qweight, absmax, absmax32, m, n, code)
         if out is not None:
             return out
     dev = qweight.device
@@ -258,11 +270,12 @@ def triton_dequantize_nf4(module) -> torch.Tensor:
     qweight = weight if isinstance(weight, torch.Tensor) else weight.data
     m, n = int(module.out_features), int(module.in_features)
     dtype = quant_state.dtype
-    if _EXT is not None:
+    ext = _EXT if _EXT_READY else _ext()
+    if ext is not None:
         code = _DTYPE_CODE.get(dtype)
         if code is not None:
             # common call straight to the tensor-level entry (None = general path)
-            out = _EXT.dequant_ref(qweight, quant_state.absmax, absmax32, m, n, code)
+            out = ext.dequant_ref(qweight, quant_state.absmax, absmax32, m, n, code)
             if out is not None:
                 return out
     return _dequantize(weight.data, quant_state.absmax, absmax32, dtype, m, n)

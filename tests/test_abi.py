@@ -124,6 +124,50 @@ def test_tensor_fast_entry_loads_and_declines_host_tensors():
     from nf4_triton_dequantization_amd import kernel
 
     E = _lib.ext()
-    assert E is not None and kernel._EXT is E
+    assert E is not None and kernel._ext() is E
     q = torch.zeros(64, dtype=torch.uint8)
     assert E.dequant_ref(q, torch.ones(2, dtype=torch.uint8), torch.ones(1), 2, 64, _lib.BF16) is None
+
+
+def _run_py(code, **env):
+    import os
+    import subprocess
+    import sys
+
+    e = dict(os.environ, **env)
+    return subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120,
+                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def test_import_without_library_then_loud_failure():
+    """Importing the package loads no native code: the pure-Python helpers (quantizer,
+    checkpoint layout) work without libnf4dq.so, and the first compute call raises."""
+    code = (
+        "import torch, types\n"
+        "import nf4_triton_dequantization_amd as P\n"
+        "from nf4_triton_dequantization_amd import bnb_layout\n"
+        "w = torch.randn(4, 64)\n"
+        "bnb_layout.quantize_nf4(w)\n"
+        "from nf4_triton_dequantization import triton_dequantize_nf4\n"
+        "qs = types.SimpleNamespace(absmax=torch.zeros(4, dtype=torch.uint8), dtype=torch.bfloat16,\n"
+        "    state2=types.SimpleNamespace(absmax=torch.ones(1)))\n"
+        "mod = types.SimpleNamespace(weight=types.SimpleNamespace(data=torch.zeros(128, 1, dtype=torch.uint8),\n"
+        "    quant_state=qs), out_features=4, in_features=64)\n"
+        "try:\n"
+        "    triton_dequantize_nf4(mod)\n"
+        "except RuntimeError as e:\n"
+        "    assert 'not built' in str(e), e\n"
+        "    print('raised')\n"
+    )
+    r = _run_py(code, NF4DQ_LIB_PATH="/nonexistent/libnf4dq.so")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "raised"
+
+
+def test_diagnostic_lib_path_skips_tensor_entry():
+    """With NF4DQ_LIB_PATH set, nf4ext.so (linked to the product build) is not loaded,
+    so every call goes to the selected build; a broken ext file only warns."""
+    r = _run_py("from nf4_triton_dequantization_amd import _lib; print(_lib.ext())",
+                NF4DQ_LIB_PATH=_lib.LIB_PATH)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "None"

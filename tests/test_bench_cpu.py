@@ -30,7 +30,8 @@ def _json(stdout):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("n", [2, 3])
 def test_gpus_flag_spawns_ranks(n):
-    p = _run(["--gpus", str(n), "--backend", "cpu", "--steps", "2", "--warmup", "1", "--m", "64", "--n", "128"])
+    p = _run(["--gpus", str(n), "--backend", "cpu", "--steps", "2", "--warmup", "1", "--m", "64", "--n", "128",
+              "--c5-shape", "64x128", "--cpu-seconds", "0.2"])
     assert p.returncode == 0, p.stderr[-3000:]
     d = _json(p.stdout)
     assert d["n_gpus"] == n and len(d["per_rank"]) == n
@@ -39,15 +40,46 @@ def test_gpus_flag_spawns_ranks(n):
     slowest = max(r["ms_per_step"] for r in d["per_rank"])
     assert d["ms_per_step"] == pytest.approx(slowest)
     assert d["value"] == pytest.approx(n * 64 * 128 / (slowest * 1e-3), rel=1e-6)
+    # the host-CPU baseline is on the line at every N (rank 0, after the timed regions)
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["native"]["value"] > 0 and cb["cores"] >= 1
+    # BASELINE configs[4] at this N: 8 matrices split round-robin, per-rank and aggregate
+    # figures, the quant statistics scattered (each rank got only its own share)
+    c5 = d["c5"]
+    assert c5["matrices"] == 8 and c5["n_gpus"] == n and c5["scaling"] == "strong"
+    assert [r["matrices"] for r in c5["per_rank"]] == [len(range(r, 8, n)) for r in range(n)]
+    c5_slowest = max(r["ms_per_step"] for r in c5["per_rank"])
+    assert c5["ms_per_step"] == pytest.approx(c5_slowest)
+    assert c5["elements_per_s"] == pytest.approx(8 * 64 * 128 / (c5_slowest * 1e-3), rel=1e-6)
+    assert c5["GBps"] > 0 and all(r["GBps"] > 0 and r["elements_per_s"] > 0 for r in c5["per_rank"])
+    assert c5["quant_state_scatter_ms"] >= 0
+    per_matrix = 64 * 128 // 64 + 4 * ((64 * 128 // 64 + 255) // 256)
+    assert c5["quant_state_bytes_per_rank"] == [per_matrix * len(range(r, 8, n)) for r in range(n)]
+    assert c5["verified_first_rows"] is True
+    assert c5["cpu_baseline"]["native"] > 0 and c5["cpu_baseline"]["value"] > 0
 
 
 @pytest.mark.timeout(300)
 def test_c5_split_over_ranks():
-    p = _run(["--gpus", "2", "--backend", "cpu", "--workload", "c5", "--steps", "1", "--warmup", "0", "--sets", "1"])
+    p = _run(["--gpus", "2", "--backend", "cpu", "--workload", "c5", "--steps", "1", "--warmup", "0", "--sets", "1",
+              "--no-cpu-baseline"])
     assert p.returncode == 0, p.stderr[-3000:]
     d = _json(p.stdout)
     assert d["scaling"] == "strong" and d["config"]["matrices_per_rank"] == 4
     assert d["value"] == pytest.approx(8 * 8192 * 8192 / (d["ms_per_step"] * 1e-3), rel=1e-6)
+
+
+@pytest.mark.timeout(120)
+def test_failing_rank_stops_the_others():
+    """A rank that dies early ends the launch at once (the others would otherwise wait
+    in the rendezvous until the backend timeout)."""
+    import time
+
+    t0 = time.time()
+    p = _run(["--gpus", "2", "--backend", "cpu", "--steps", "1", "--m", "64", "--n", "128", "--no-cpu-baseline"],
+             env_extra={"NF4_BENCH_FAIL_RANK": "1"}, timeout=110)
+    assert p.returncode != 0 and "failing on request" in p.stderr
+    assert time.time() - t0 < 100
 
 
 def test_world_size_must_match_gpus():

@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from nf4_triton_dequantization_amd.sharding import (QuantStats, assign_round_robin, broadcast_quant_stats,
-                                                    max_over_ranks)
+                                                    max_over_ranks, scatter_quant_stats)
 
 
 def _free_port():
@@ -80,3 +80,44 @@ def test_round_robin_covers_everything():
             assert max(len(p) for p in parts) - min(len(p) for p in parts) <= 1
     with pytest.raises(ValueError):
         assign_round_robin(3, 0)
+
+
+def _scatter_worker(rank, world, port, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ref = _stats(7)
+        owned = assign_round_robin(len(ref), world)
+        per_rank = [[ref[i] for i in owned[r]] for r in range(world)] if rank == 0 else None
+        got = scatter_quant_stats(per_rank, torch.device("cpu"), src=0)
+        want = [ref[i] for i in owned[rank]]
+        ok = len(got) == len(want) and all(
+            a.m == b.m and a.n == b.n and a.dtype == b.dtype and torch.equal(a.absmax, b.absmax)
+            and torch.equal(a.absmax2, b.absmax2) for a, b in zip(got, want))
+        # a rank that owns nothing gets an empty list
+        empty = scatter_quant_stats([[] for _ in range(world)] if rank == 0 else None, torch.device("cpu"), src=0)
+        result_q.put((rank, ok, len(got), sum(int(s.absmax.numel()) for s in got), len(empty)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("world", [2, 3])
+def test_scatter_sends_each_rank_only_its_own(world):
+    """scatter_quant_stats: each rank receives exactly its round-robin share (uneven at
+    world 3: 3/2/2 matrices), bit-equal, and nothing else."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=90) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    ref = _stats(7)
+    owned = assign_round_robin(7, world)
+    for r, ok, k, nbytes, nempty in res:
+        assert ok and k == len(owned[r]) and nempty == 0
+        assert nbytes == sum(int(ref[i].absmax.numel()) for i in owned[r])

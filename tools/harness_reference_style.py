@@ -147,7 +147,9 @@ def main():
     # the pieces: the tensor-level entry alone (no Python attribute reads), and the
     # bare C-ABI launch into a preallocated output through ctypes
     from nf4_triton_dequantization_amd import _lib
-    from nf4_triton_dequantization_amd.kernel import _EXT
+    from nf4_triton_dequantization_amd import kernel as _K
+
+    _EXT = _K._ext()
 
     qs = w.quant_state
     q, a1, a2 = w.data, qs.absmax, qs.state2.absmax

@@ -1,0 +1,71 @@
+#!/bin/bash
+# One parametrised GPU-box session (replaces the per-call tools/_run*.sh scripts of
+# rounds 1-2, which are in git history).  Usage, on the box:
+#   bash tools/session.sh <out-subdir> <stage> [<stage> ...]
+# Every stage writes under gpurun_out/<out-subdir>/; every GPU step runs under its
+# own time limit and the session stops at the first failing step.
+set -e -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/$1
+shift
+mkdir -p "$O"
+PY="python -u"
+
+trace() {  # trace <name> <kernel-substring> <last-K> <timeout> -- <python args...>
+    local name=$1 kern=$2 k=$3 to=$4
+    shift 5
+    timeout -k 10 "$to" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$name" -o "$name" -- \
+        python3 -u "$@" > "$O/$name.out" 2> "$O/$name.err"
+    python3 tools/trace_gaps.py "$O/prof_$name" "$kern" "$k" > "$O/${name}_gaps.txt"
+    tail -1 "$O/${name}_gaps.txt"
+}
+
+for stage in "$@"; do
+    echo "== stage $stage" >&2
+    case $stage in
+    gputest)
+        timeout -k 10 900 $PY -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+            > "$O/gputest.log" 2>&1 || { tail -30 "$O/gputest.log"; exit 1; }
+        tail -3 "$O/gputest.log" ;;
+    smoke)
+        timeout -k 10 300 $PY __graft_entry__.py smoke > "$O/smoke.log" 2>&1; cat "$O/smoke.log" ;;
+    bench)
+        timeout -k 10 300 $PY bench.py > "$O/bench.json" 2> "$O/bench.err"; cat "$O/bench.json" ;;
+    bench20)
+        timeout -k 10 200 $PY bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$O/bench_k20.json" 2>> "$O/bench.err"
+        cat "$O/bench_k20.json" ;;
+    multirank)  # N ranks on the one GPU of a lease (gloo; the driver's 8-GPU node runs RCCL)
+        timeout -k 10 400 $PY bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 > "$O/bench_g2_gloo.json" 2> "$O/bench_g2.err"
+        cat "$O/bench_g2_gloo.json" ;;
+    c5probe)
+        timeout -k 10 400 $PY tools/c5_probe.py > "$O/c5_probe.jsonl" 2> "$O/c5_probe.err"; cat "$O/c5_probe.jsonl" ;;
+    valsens)
+        timeout -k 10 300 $PY tools/value_sensitivity.py > "$O/value_sensitivity.jsonl" 2> "$O/vs.err"
+        cat "$O/value_sensitivity.jsonl" ;;
+    c5bench)
+        timeout -k 10 200 $PY bench.py --m 8192 --n 8192 --steps 64 --no-cpu-baseline > "$O/bench_8192.json" 2> "$O/bench_8192.err"
+        timeout -k 10 200 $PY bench.py --workload c5 --steps 20 --no-cpu-baseline > "$O/bench_c5.json" 2> "$O/bench_c5.err"
+        timeout -k 10 600 $PY tools/bench_configs.py --configs c5 > "$O/configs_c5.jsonl" 2> "$O/configs_c5.err"
+        cat "$O/bench_8192.json" "$O/bench_c5.json" "$O/configs_c5.jsonl" ;;
+    c5knobs)  # launch-shape variants at 8192^2 (eager, per-set absmax): KNOBS="label:args;label:args"
+        IFS=';' read -ra KS <<< "${KNOBS:-default:;bpc8:--blocks-per-cu 8;bpc8_a1ahead:--blocks-per-cu 8 --flags 8;bpc4_a1ahead:--blocks-per-cu 4 --flags 8;bpc16_a1ahead:--blocks-per-cu 16 --flags 8;u8:--tile-dwords 8}"
+        for kv in "${KS[@]}"; do
+            lab=${kv%%:*}; a=${kv#*:}
+            timeout -k 10 200 $PY bench.py --m 8192 --n 8192 --steps 64 --no-cpu-baseline $a > "$O/knob_$lab.json" 2>> "$O/knobs.err"
+            python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['roofline']['launch_us_mean'],3), round(d['roofline']['frac'],4))" "$O/knob_$lab.json" "$lab"
+        done ;;
+    c5trace)
+        trace configs_c5 nf4_flat_kernel 32 600 -- tools/bench_configs.py --configs c5
+        trace bench_8192 nf4_flat_kernel 64 300 -- bench.py --m 8192 --n 8192 --steps 64 --no-cpu-baseline ;;
+    rocprof)
+        trace bench nf4_flat_kernel 200 300 -- bench.py --steps 200 --no-cpu-baseline
+        python3 tools/rocprof_summary.py "$O/prof_bench" nf4_flat_kernel "$O/rocprof_bench_summary.json" \
+            "$O/rocprof_bench_kernel_stats.csv" --last 200 > /dev/null ;;
+    configs)
+        timeout -k 10 900 $PY tools/bench_configs.py > "$O/configs.jsonl" 2> "$O/configs.err"; cat "$O/configs.jsonl" ;;
+    *)
+        echo "unknown stage $stage" >&2; exit 2 ;;
+    esac
+done
+echo "session done" >&2
