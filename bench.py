@@ -32,8 +32,9 @@ the GPU TLB for every set.  ``--launch graph`` captures the K steps into one
 hipGraph instead: on ROCm 7.2 a replay carries a fixed ~7-10 us outside the
 kernels (rocprof: 20 launches span 139 us, the events 149 us), 0.4-0.5 us per
 step at the driver's K = 20 (A/B: profiles/r02/bench_eager_ab.txt).  Step i uses
-buffer set i % P; P is chosen so each rank's sets span >= 1 GiB (>> the 256 MiB
-Infinity Cache) and so that a set is reused >= 256 MiB of traffic later across
+buffer set i % P; P is chosen so each rank's sets span >= 512 MiB (2x the 256 MiB
+Infinity Cache; >= 512 MiB, in the flat HBM regime -- MIN_FOOTPRINT) and, under
+graph replay, so that a set is reused >= 256 MiB of traffic later across
 the untimed -> timed boundary (profiles/r02/bench_ab.txt: a scratch-write flush
 instead costs 1-2 us per step through TLB misses).  ``value`` = elements of all
 ranks / max over ranks of the region time.
@@ -79,7 +80,12 @@ sys.path.insert(0, REPO)
 
 PEAK_HBM = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
 ROUNDS = ("r02", "r01")  # profiles/<round>/pmc_traffic.json, newest first
-MIN_FOOTPRINT = 1 << 30  # bytes of buffer sets per rank (>> 256 MiB Infinity Cache)
+# bytes of buffer sets per rank: 2x the 256 MiB Infinity Cache.  The per-launch time is
+# flat from ~300 MB to ~1.1 GB of rotating sets (the HBM-streaming regime: 4096^2 6.93-6.95
+# us at 7..26 sets), lower below it (Infinity Cache hits: 6.39 us at 2 sets) and ~5-10 %
+# higher past ~1.2 GB (7.25 us at 29 sets; 8192^2 24.7 us at 7 sets vs 27.1-27.5 at 8..14):
+# profiles/r03/c5/footprint_*.jsonl.  512 MiB sits mid-plateau.
+MIN_FOOTPRINT = 512 << 20
 
 
 def log(*a):
@@ -95,7 +101,7 @@ def parse_args(argv=None):
     ap.add_argument("--m", type=int, default=None, help="override the c2 matrix shape (rows)")
     ap.add_argument("--n", type=int, default=None, help="override the c2 matrix shape (columns)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
-    ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = enough for >= 1 GiB)")
+    ap.add_argument("--sets", type=int, default=0, help="rotating buffer sets (0 = enough for >= 512 MiB)")
     ap.add_argument("--launch", default="eager", choices=["eager", "graph"],
                     help="timed steps as eager C-ABI launches (default) or one hipGraph replay")
     ap.add_argument("--no-graph", action="store_true", help="same as --launch eager (kept for old scripts)")
@@ -109,7 +115,8 @@ def parse_args(argv=None):
     ap.add_argument("--tile-dwords", type=int, default=4)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=1)
-    ap.add_argument("--flags", type=int, default=0, help="NF4DQ_CFG_* bits (1 = nt loads)")
+    ap.add_argument("--flags", type=lambda v: int(v, 0), default=0,
+                    help="nf4_launch_cfg.flags: (log2 absmax prefetch distance in tiles) << 8, 0 = off")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])
@@ -292,13 +299,17 @@ class Workload:
         self.mats, self.cpu, self.code = mats, cpu, code
         self.L = _lib.lib()
         step_bytes = sum(m * n // 2 + 2 * m * n for _, m, n in mats)  # packed + output per step
-        P = args.sets or max(2, -(-MIN_FOOTPRINT // max(1, step_bytes)))
+        # (a step that alone spans >= MIN_FOOTPRINT -- c5's 8 matrices on one GPU -- needs
+        # no second set: its own bytes push it out of the Infinity Cache before it recurs)
+        P = args.sets or max(1, -(-MIN_FOOTPRINT // max(1, step_bytes)))
         if cpu:
             P = args.sets or 2
-        elif not args.sets:
-            # across the untimed -> timed boundary set 0 is reused after
+        elif not args.sets and args.launch == "graph" and not args.no_graph:
+            # graph replay: across the boundary between two replays set 0 is reused after
             # K - P*floor((K-1)/P) steps (K when P >= K): keep that >= 256 MiB so no set
-            # is still in the Infinity Cache when a timed step reaches it
+            # is still in the Infinity Cache when a timed step reaches it.  (Eager: the
+            # untimed lead launches walk every set in order, so a set recurs after P - 1
+            # others -- >= 512 MiB -- already.)
             def reuse(p):
                 return args.steps if p >= args.steps else args.steps - p * ((args.steps - 1) // p)
 

@@ -114,25 +114,13 @@ int nf4_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t n
                            int32_t blocksize, void* hip_stream);
 
 /* Launch tuning (bench/tuning only; the entry points above use the default
- * {4, 0, 1, 0}).  tile_dwords: 4 or 8 packed dwords per lane per tile;
- * blocks_per_cu: grid cap per CU (0 = one wave per tile, no cap); nontemporal:
- * 0 = default-policy output stores, 1 = streaming (sc1+nt) stores; flags: NF4DQ_CFG_* bits.  Non-default
- * tile/nt-load/workgroup settings exist for fp16/bf16 reference semantics. */
-#define NF4DQ_CFG_NT_LOADS 1   /* nt cache policy on the packed-weight loads */
-#define NF4DQ_CFG_X4_LOADS 2   /* 16 B/lane packed loads, redistributed through LDS */
-#define NF4DQ_CFG_X4_DIRECT 4  /* 16 B/lane packed loads, four strided 16 B stores per lane (no LDS) */
-#define NF4DQ_CFG_A1_AHEAD 8   /* absmax bytes loaded one tile ahead of the packed loads */
-/* bits 8..11: log2 of the number of contiguous tile segments (0..6); block b
- * works in segment b % 2^k (k = 3: one segment per XCD under round-robin placement) */
-#define NF4DQ_CFG_SEG_SHIFT_BIT 8
-#define NF4DQ_CFG_SEG_SHIFT_MASK 0xF00
-/* bits 4..7: log2 of waves per workgroup (0 = default 4; 1, 2, 3, 4 = 2, 4, 8, 16) */
-#define NF4DQ_CFG_WG_SHIFT_BIT 4
-#define NF4DQ_CFG_WG_SHIFT_MASK 0xF0
-/* bits 12..15: output-store cache policy experiment (0 = default sc1+nt; 1 nt,
- * 2 sc0+nt, 3 sc0+sc1+nt, 4 sc1, 5 sc0+sc1); base tile shape only */
-#define NF4DQ_CFG_STORE_POLICY_BIT 12
-#define NF4DQ_CFG_STORE_POLICY_MASK 0xF000
+ * {4, 0, 1, 0}).  tile_dwords must be 4 and nontemporal 1 (the tile shape and
+ * the sc1+nt output stores every entry point uses; the other shapes and store
+ * policies measured slower and were removed, profiles/r01/tune_sweep.log,
+ * profiles/r02/x4_direct/).  blocks_per_cu: grid cap per CU (0 = one wave per
+ * tile, no cap; capped grids walk tiles persistently).  flags: reserved, 0.
+ * (Absmax-line and page-translation prefetches were tried as flags and measured
+ * no better than 1 %, profiles/r03/c5/; removed.) */
 typedef struct nf4_launch_cfg {
     int32_t tile_dwords;
     int32_t blocks_per_cu;
@@ -154,10 +142,11 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len,
  * NF4DQ_ERR_SHAPE): M <= NF4DQ_GEMM_MAX_M, N % 64 == 0, K % 128 == 0,
  * packed_len == N*K/2 (and N <= 2^18).  `workspace` (16-byte aligned) must hold
  * nf4_gemm_workspace_bytes(M, N, K) bytes (0 = none needed): split-K ticket
- * counters + fp32 partials, reduced inside the launch in a fixed order
+ * counters + 64-bit partial-sum entries, handed between workgroups with relaxed
+ * agent-scope atomics only and reduced inside the launch in a fixed order
  * (bitwise reproducible).  The workspace must be ZERO-FILLED before its first
- * use; every call leaves it reusable (counters back to 0).  One workspace per
- * stream: concurrent calls must not share one. */
+ * use; every call leaves it reusable (counters and entries back to 0).  One
+ * workspace per stream: concurrent calls must not share one. */
 #define NF4DQ_GEMM_MAX_M 32
 size_t nf4_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len,

@@ -62,7 +62,6 @@ class LaunchCfg(ctypes.Structure):
     ]
 
 
-CFG_NT_LOADS = 1
 GEMM_K128 = 1
 GEMM_STREAM = 2
 GEMM_PERSIST = 3

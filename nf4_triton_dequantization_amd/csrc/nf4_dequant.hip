@@ -73,7 +73,6 @@ struct Batch {
     Desc d[MAXB];
     uint32_t count;
     uint32_t total_tiles;
-    uint32_t seg_shift;  // tiles are split into 2^seg_shift contiguous segments, one per block residue
 #if NF4_FLAT_STAMPS
     unsigned long long* stamps;
 #endif
@@ -83,7 +82,7 @@ struct Batch {
 #define NF4_FSTAMP(slot_, val_)                                                                      \
     do {                                                                                             \
         __builtin_amdgcn_sched_barrier(0);                                                           \
-        if (lane == 0) bt.stamps[(blockIdx.x * WPG + (threadIdx.x >> 6)) * 4u + (slot_)] = (val_);   \
+        if (lane == 0) bt.stamps[(blockIdx.x * kWaves + (threadIdx.x >> 6)) * 4u + (slot_)] = (val_); \
         __builtin_amdgcn_sched_barrier(0);                                                           \
     } while (0)
 #define NF4_FNOW() __builtin_amdgcn_s_memrealtime()
@@ -106,13 +105,14 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
     }
 }
 
-constexpr int kWg = 256;  // 4 waves (rows / bytes kernels; the flat kernel takes WPG)
+constexpr int kWg = 256;   // 4 waves per workgroup (every kernel here)
+constexpr int kWaves = 4;
+constexpr int kU = 4;      // packed dwords (fp32 output: words) per lane per tile
 
 // Cache-policy bits of the buffer instructions (aux operand, gfx950 CPol):
-// 1 = sc0, 2 = nt (streaming), 16 = sc1.  Output stores default to sc1+nt
-// (write-once stream, not kept in the XCD L2: measured 1-2 % faster per launch
-// than nt alone and a cheaper end-of-kernel write-back).
-constexpr int kAuxNt = 2;
+// 2 = nt (streaming), 16 = sc1.  Output stores are sc1+nt: a write-once stream,
+// not kept in the XCD L2 (+25-30 % over default-policy stores, and 1-2 % over nt
+// alone; profiles/r01/tune_sweep.log).
 constexpr int kAuxStore = 18;
 
 template <int DT>
@@ -122,24 +122,20 @@ constexpr uint32_t out_bytes_per_packed_byte() { return DT == NF4DQ_F32 ? 8u : 4
 // per step and a wave store instruction covers 1 KiB contiguous.
 template <int DT>
 constexpr uint32_t lane_bytes() { return DT == NF4DQ_F32 ? 2u : 4u; }
-template <int DT, int U>
-constexpr uint32_t tile_bytes() { return 64u * lane_bytes<DT>() * U; }
+template <int DT>
+constexpr uint32_t tile_bytes() { return 64u * lane_bytes<DT>() * kU; }
 
 // Raw inputs of one wave-tile, loaded ahead of use (software pipeline stage 1).
-template <int U>
 struct TileIn {
-    uint32_t w[U];  // U packed dwords of this lane
-    uint32_t a1;    // raw absmax byte of this lane's scale block (ref / bnb)
-    float a2;       // nested absmax (ref / bnb) or fp32 absmax (single modes)
-    float c2;       // bnb: code2[a1] (loaded after a1)
+    uint32_t w[kU];  // packed dwords of this lane
+    uint32_t a1;     // raw absmax byte of this lane's scale block (ref / bnb)
+    float a2;        // nested absmax (ref / bnb) or fp32 absmax (single modes)
 };
 
-// Issue the loads of tile `base` (packed bytes) of matrix D.  Buffer loads
-// outside the matrix return 0, so partial tiles need no predicates.
 // Block index (within the whole matrix / stream) of this lane's scale block in tile `base`.
-template <int DT, int U>
+template <int DT>
 __device__ __forceinline__ uint32_t tile_block(const Desc& D, uint32_t base, uint32_t lane) {
-    constexpr uint32_t kTileBytes = tile_bytes<DT, U>();
+    constexpr uint32_t kTileBytes = tile_bytes<DT>();
     const uint32_t bsh = D.blk_shift;
     const uint32_t bpt = kTileBytes >> bsh;  // 0 when one block spans the tile
     uint32_t g = (base >> bsh) + (bpt ? (lane & (bpt - 1u)) : 0u);
@@ -148,41 +144,24 @@ __device__ __forceinline__ uint32_t tile_block(const Desc& D, uint32_t base, uin
     return g + D.blk_base;
 }
 
-// Reference mode: the absmax byte of tile `base` on its own, issued a tile ahead of
-// the tile's packed loads (A1A kernels) -- the 1-byte gathers come from a different
-// DRAM row than the packed stream and, issued with it, are the tile's last arrival.
-template <int DT, int U>
-__device__ __forceinline__ uint32_t a1_load(const Desc& D, uint32_t base, uint32_t lane) {
-    return D.a1[fmodu(tile_block<DT, U>(D, base, lane), D.nb)];
-}
-
-template <int DT, int MODE, int U, int AUXL, int X4 = 0, int LOADA1 = 1>
-__device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rsrc_t rp, uint32_t base,
-                                               uint32_t lane) {
+// Issue the loads of tile `base` (packed bytes) of matrix D.  Buffer loads
+// outside the matrix return 0, so partial tiles need no predicates.
+template <int DT, int MODE>
+__device__ __forceinline__ TileIn tile_load(const Desc& D, __amdgpu_buffer_rsrc_t rp, uint32_t base, uint32_t lane) {
     constexpr uint32_t LB = lane_bytes<DT>();
-    TileIn<U> in;
-    if constexpr (X4) {
-        // one 16-byte load per lane (1 KiB per wave instruction); tile_finish
-        // redistributes through LDS into the store-friendly dword order
-        static_assert(U == 4 && LB == 4, "x4 loads: base tile shape only");
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rp, base + 16u * lane, 0, AUXL);
-        in.w[0] = v.x;
-        in.w[1] = v.y;
-        in.w[2] = v.z;
-        in.w[3] = v.w;
-    } else
+    TileIn in;
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
+    for (int j = 0; j < kU; ++j) {
         const uint32_t off = base + 64u * LB * j + LB * lane;
         if constexpr (LB == 4) {
-            in.w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, AUXL);
+            in.w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 0);
         } else {
-            in.w[j] = __builtin_amdgcn_raw_buffer_load_b16(rp, off, 0, AUXL);
+            in.w[j] = __builtin_amdgcn_raw_buffer_load_b16(rp, off, 0, 0);
         }
     }
-    const uint32_t g = tile_block<DT, U>(D, base, lane);
+    const uint32_t g = tile_block<DT>(D, base, lane);
     if constexpr (MODE == kRef) {
-        if constexpr (LOADA1) in.a1 = D.a1[fmodu(g, D.nb)];
+        in.a1 = D.a1[fmodu(g, D.nb)];
         const uint32_t r = fdiv(g, D.bpr);
         const uint32_t b = g - r * D.bpr.d;
         in.a2 = D.a2[fmodu(r * D.groups + (b >> 2), D.n2)];
@@ -200,22 +179,12 @@ __device__ __forceinline__ TileIn<U> tile_load(const Desc& D, __amdgpu_buffer_rs
 }
 
 // Stage 2: scale of this lane's block, ds_bpermute to the dword owners, decode,
-// round, and U 16-byte stores (fp32: 2U) -- each wave store instruction writes
-// 1 KiB contiguous; stores past the end of the matrix are dropped by the buffer
-// range check.
-template <int DT, int MODE, int U, int AUXS, int X4 = 0>
+// round, and kU 16-byte stores -- each wave store instruction writes 1 KiB
+// contiguous; stores past the end of the matrix are dropped by the buffer range
+// check.
+template <int DT, int MODE>
 __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_t ro, const float* lut,
-                                            const TileIn<U>& in_, uint32_t base, uint32_t lane,
-                                            uint32_t* stage = nullptr, const float* code2s = nullptr) {
-    TileIn<U> in = in_;
-    if constexpr (X4 == 1) {
-        // lane l holds packed bytes [16l, 16l+16); the store layout wants dword
-        // j of lane l = bytes [256j + 4l, +4).  One ds_write_b128 + four
-        // ds_read_b32 on this wave's private 1 KiB slice (in-order per wave).
-        reinterpret_cast<u32x4*>(stage)[lane] = u32x4{in.w[0], in.w[1], in.w[2], in.w[3]};
-#pragma unroll
-        for (int j = 0; j < U; ++j) in.w[j] = stage[64 * j + lane];
-    }
+                                            const TileIn& in, uint32_t base, uint32_t lane, const float* code2s) {
     float s;
     if constexpr (MODE == kRef) {
         s = ((float)in.a1 / 127.0f) * in.a2;  // IEEE division (:45, :270), then fp32 multiply
@@ -230,10 +199,8 @@ __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_
     constexpr uint32_t kOB = out_bytes_per_packed_byte<DT>();
     constexpr uint32_t LB = lane_bytes<DT>();
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-        // X4 == 2 (direct): dword j of lane l is packed bytes [16l + 4j, +4), stored
-        // where it came from (four 16 B stores per lane, each instruction strided by 64 B)
-        const uint32_t rel = X4 == 2 ? 16u * lane + 4u * j : 64u * LB * j + LB * lane;
+    for (int j = 0; j < kU; ++j) {
+        const uint32_t rel = 64u * LB * j + LB * lane;
         const float sj = __shfl(s, (int)(rel >> bsh), 64);
         const uint32_t w = in.w[j];
         const uint32_t hi4 = (w >> 2) & 0x3C3C3C3Cu;
@@ -248,10 +215,10 @@ __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_
         const uint32_t ob = (base + rel) * kOB;
         if constexpr (DT == NF4DQ_F32) {
             u32x4 o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-            __builtin_amdgcn_raw_buffer_store_b128(o, ro, ob, 0, AUXS);
+            __builtin_amdgcn_raw_buffer_store_b128(o, ro, ob, 0, kAuxStore);
         } else {
             u32x4 o = {pack2<DT>(v[0], v[1]), pack2<DT>(v[2], v[3]), pack2<DT>(v[4], v[5]), pack2<DT>(v[6], v[7])};
-            __builtin_amdgcn_raw_buffer_store_b128(o, ro, ob, 0, AUXS);
+            __builtin_amdgcn_raw_buffer_store_b128(o, ro, ob, 0, kAuxStore);
         }
     }
 }
@@ -264,32 +231,22 @@ __device__ __forceinline__ uint32_t find_matrix(const Batch<MAXB>& bt, uint32_t 
     return k;
 }
 
-// Position of a wave in the launch: the i-th tile of its segment, which is
-// tile t of the launch = tile of matrix k starting at packed byte `base`.
+// Position of a wave in the launch: tile t of the launch = tile of matrix k
+// starting at packed byte `base`.
 struct Cursor {
-    uint32_t i, t, k, base;
+    uint32_t t, k, base;
     bool valid;
 };
 
-// Segments: block b works in segment b % S (S = 2^seg_shift, the grid is a
-// multiple of S), so with S = 8 and the observed round-robin block placement
-// each XCD sweeps one contiguous region instead of all eight interleaving
-// through the same window (speed only: any placement is correct).
-struct SegMap {
-    uint32_t seg_base;  // first tile of this block's segment
-    uint32_t seg_tiles; // tiles per segment (last segment may be shorter)
-};
-
-template <int DT, int U, int MAXB>
-__device__ __forceinline__ Cursor cursor_at(const Batch<MAXB>& bt, const SegMap& sm, uint32_t i, uint32_t k_hint) {
-    constexpr uint32_t kTileBytes = tile_bytes<DT, U>();
+template <int DT, int MAXB>
+__device__ __forceinline__ Cursor cursor_at(const Batch<MAXB>& bt, uint32_t t, uint32_t k_hint) {
+    constexpr uint32_t kTileBytes = tile_bytes<DT>();
     Cursor c;
-    c.i = i;
-    c.t = sm.seg_base + i;
-    c.valid = i < sm.seg_tiles && c.t < bt.total_tiles;
-    c.k = c.valid ? find_matrix(bt, c.t, k_hint) : k_hint;
+    c.t = t;
+    c.valid = t < bt.total_tiles;
+    c.k = c.valid ? find_matrix(bt, t, k_hint) : k_hint;
     // past the end: an offset beyond every buffer range (loads return 0, stores drop)
-    c.base = c.valid ? (c.t - bt.d[c.k].tile_begin) * kTileBytes : 0xFFFFF000u;
+    c.base = c.valid ? (t - bt.d[c.k].tile_begin) * kTileBytes : 0xFFFFF000u;
     return c;
 }
 
@@ -302,53 +259,40 @@ __device__ __forceinline__ void make_rsrcs(const Batch<MAXB>& bt, uint32_t k, __
 }
 
 // Persistent, software-pipelined flat kernel.  Each wave walks tiles
-// t, t + nwaves, ...; the loop is unrolled by two with the tiles in two
-// register sets (A, B) so that tile i+1's loads are in flight while tile i is
-// decoded and stored, with no register copies (a copy would force a wait on
-// the loads it copies).
-template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB, int X4 = 0, int A1A = 0>
-__global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt) {
-    static_assert(!A1A || MODE == kRef, "absmax bytes ahead: reference semantics");
+// t, t + nwaves, ... (one tile per wave unless the grid is capped); the loop is
+// unrolled by two with the tiles in two register sets (A, B) so that tile i+1's
+// loads are in flight while tile i is decoded and stored, with no register copies
+// (a copy would force a wait on the loads it copies).
+template <int DT, int MODE, int MAXB>
+__global__ __launch_bounds__(kWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
     __shared__ __attribute__((aligned(16))) float lut[16];
     __shared__ __attribute__((aligned(16))) float code2s[MODE == kBnb ? 256 : 1];  // bitsandbytes code (every piece's)
-    __shared__ __attribute__((aligned(16))) uint32_t stage_all[X4 ? WPG * 256 : 1];
-    uint32_t* stage = stage_all + (X4 ? (threadIdx.x >> 6) * 256 : 0);
     const uint32_t lane = threadIdx.x & 63u;
 #if NF4_FLAT_STAMPS
     const unsigned long long t_entry = NF4_FNOW();
     unsigned long long tiles_done = 0;
 #endif
-    const uint32_t sshift = bt.seg_shift;
-    SegMap sm;
-    sm.seg_tiles = (bt.total_tiles + (1u << sshift) - 1u) >> sshift;
-    sm.seg_base = (blockIdx.x & ((1u << sshift) - 1u)) * sm.seg_tiles;
-    const uint32_t i0 = __builtin_amdgcn_readfirstlane((blockIdx.x >> sshift) * WPG + (threadIdx.x >> 6));
-    const uint32_t nwaves = (gridDim.x >> sshift) * WPG;  // waves per segment
+    const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * kWaves;
 
     // First tile's loads go out before anything else (a wave without work
     // issues them past the buffer range: no traffic); the LUT write and the
     // barrier then overlap their latency.
-    Cursor ca = cursor_at<DT, U>(bt, sm, i0, 0u);
+    Cursor ca = cursor_at<DT>(bt, t0, 0u);
     __amdgpu_buffer_rsrc_t rpa, roa;
     make_rsrcs<DT>(bt, ca.k, rpa, roa);
-    TileIn<U> A = tile_load<DT, MODE, U, AUXL, X4>(bt.d[ca.k], rpa, ca.base, lane);
-    uint32_t a1n = 0;  // A1A: absmax bytes of the wave's next tile
-    if constexpr (A1A) {
-        const Cursor c1 = cursor_at<DT, U>(bt, sm, i0 + nwaves, ca.k);
-        a1n = a1_load<DT, U>(bt.d[c1.k], c1.base, lane);
-    }
+    TileIn A = tile_load<DT, MODE>(bt.d[ca.k], rpa, ca.base, lane);
     // Out-of-range (dropped) stores with the loop body's count: loop entry then
     // looks like the back edge to hipcc's waitcnt pass ([loads][stores]), so the
     // in-loop waits count past the previous tile's stores instead of draining them.
     {
-        constexpr int kStores = U;
         const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int j = 0; j < kStores; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, roa, 0xFFFFF000u + 16u * j, 0, AUXS);
+        for (int j = 0; j < kU; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, roa, 0xFFFFF000u + 16u * j, 0, kAuxStore);
     }
     write_lut(lut);
     if constexpr (MODE == kBnb) {  // every piece of a bitsandbytes stream carries the same code
-        for (uint32_t i = threadIdx.x; i < 256u; i += 64u * WPG) code2s[i] = bt.d[0].code2[i];
+        for (uint32_t i = threadIdx.x; i < 256u; i += kWg) code2s[i] = bt.d[0].code2[i];
     }
     __syncthreads();
     if (!ca.valid) {
@@ -359,32 +303,22 @@ __global__ __launch_bounds__(64 * WPG) void nf4_flat_kernel(const Batch<MAXB> bt
         return;
     }
     while (true) {
-        const Cursor cb = cursor_at<DT, U>(bt, sm, ca.i + nwaves, ca.k);
+        const Cursor cb = cursor_at<DT>(bt, ca.t + nwaves, ca.k);
         __amdgpu_buffer_rsrc_t rpb = rpa, rob = roa;
         if (MAXB > 1 && cb.k != ca.k) make_rsrcs<DT>(bt, cb.k, rpb, rob);
-        TileIn<U> B = tile_load<DT, MODE, U, AUXL, X4, !A1A>(bt.d[cb.k], rpb, cb.base, lane);
-        const Cursor cn = cursor_at<DT, U>(bt, sm, cb.i + nwaves, cb.k);
-        uint32_t a1m = 0;
-        if constexpr (A1A) {
-            B.a1 = a1n;
-            a1m = a1_load<DT, U>(bt.d[cn.k], cn.base, lane);
-        }
-        tile_finish<DT, MODE, U, AUXS, X4>(bt.d[ca.k], roa, lut, A, ca.base, lane, stage, code2s);
+        TileIn B = tile_load<DT, MODE>(bt.d[cb.k], rpb, cb.base, lane);
+        tile_finish<DT, MODE>(bt.d[ca.k], roa, lut, A, ca.base, lane, code2s);
 #if NF4_FLAT_STAMPS
         if (tiles_done == 0) NF4_FSTAMP(1, NF4_FNOW());
         ++tiles_done;
 #endif
         if (!cb.valid) break;
 
+        const Cursor cn = cursor_at<DT>(bt, cb.t + nwaves, cb.k);
         __amdgpu_buffer_rsrc_t rpn = rpb, ron = rob;
         if (MAXB > 1 && cn.k != cb.k) make_rsrcs<DT>(bt, cn.k, rpn, ron);
-        A = tile_load<DT, MODE, U, AUXL, X4, !A1A>(bt.d[cn.k], rpn, cn.base, lane);
-        if constexpr (A1A) {
-            A.a1 = a1m;
-            const Cursor c2 = cursor_at<DT, U>(bt, sm, cn.i + nwaves, cn.k);
-            a1n = a1_load<DT, U>(bt.d[c2.k], c2.base, lane);
-        }
-        tile_finish<DT, MODE, U, AUXS, X4>(bt.d[cb.k], rob, lut, B, cb.base, lane, stage, code2s);
+        A = tile_load<DT, MODE>(bt.d[cn.k], rpn, cn.base, lane);
+        tile_finish<DT, MODE>(bt.d[cb.k], rob, lut, B, cb.base, lane, code2s);
 #if NF4_FLAT_STAMPS
         ++tiles_done;
 #endif
@@ -492,58 +426,18 @@ int cu_count() {
     return cus;
 }
 
-// Launch one flat batch.  Tile offsets are (re)computed here for the tile size
-// of (dtype, U); callers only fill the per-matrix descriptors.  The default
-// configuration instantiates for every dtype and scale mode; the tuning knobs
-// (U = 8, nt loads, workgroup size) exist for reference semantics in fp16/bf16.
-template <int DT, int MODE, int U, int AUXS, int AUXL, int WPG, int MAXB, int X4 = 0, int A1A = 0>
+template <int DT, int MODE, int MAXB>
 void launch_one(const Batch<MAXB>& b, uint64_t blocks, hipStream_t st) {
-    hipLaunchKernelGGL((nf4_flat_kernel<DT, MODE, U, AUXS, AUXL, WPG, MAXB, X4, A1A>), dim3((unsigned)blocks),
-                       dim3(64 * WPG), 0, st, b);
+    hipLaunchKernelGGL((nf4_flat_kernel<DT, MODE, MAXB>), dim3((unsigned)blocks), dim3(kWg), 0, st, b);
 }
 
-template <int DT, int MAXB>
-int launch_tuned(const Batch<MAXB>& b, uint64_t blocks, uint32_t U, bool ntl, int wpg, hipStream_t st) {
-#define NF4_T(U_, AL_, W_) launch_one<DT, kRef, U_, kAuxStore, AL_, W_, MAXB>(b, blocks, st)
-#define NF4_W(U_, AL_)                        \
-    do {                                      \
-        if (wpg == 8) NF4_T(U_, AL_, 8);      \
-        else if (wpg == 16) NF4_T(U_, AL_, 16); \
-        else if (wpg == 2) NF4_T(U_, AL_, 2); \
-        else NF4_T(U_, AL_, 4);               \
-    } while (0)
-    if (U == 8) {
-        if (ntl) NF4_W(8, kAuxNt);
-        else NF4_W(8, 0);
-    } else if (U == 2 || U == 1) {  // finer pipeline steps (experiment): default-policy loads only
-        if (ntl) return NF4DQ_ERR_ARG;
-        if (U == 2) {
-            if (wpg == 8) NF4_T(2, 0, 8);
-            else NF4_T(2, 0, 4);
-        } else {
-            if (wpg == 8) NF4_T(1, 0, 8);
-            else NF4_T(1, 0, 4);
-        }
-    } else {
-        if (ntl) NF4_W(4, kAuxNt);
-        else NF4_W(4, 0);
-    }
-#undef NF4_W
-#undef NF4_T
-    return NF4DQ_OK;
-}
-
+// Launch one flat batch.  Tile offsets are (re)computed here for the tile size of
+// the dtype; callers only fill the per-matrix descriptors.  cfg: grid cap
+// (blocks_per_cu), validated by the caller.
 template <int MAXB>
 int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_launch_cfg& cfg, hipStream_t st) {
     if (bt.count == 0) return NF4DQ_OK;
-    const uint32_t U = cfg.tile_dwords == 8 ? 8u : cfg.tile_dwords == 2 ? 2u : cfg.tile_dwords == 1 ? 1u : 4u;
-    const bool ntl = (cfg.flags & NF4DQ_CFG_NT_LOADS) != 0;
-    const int wpg_log = (int)((cfg.flags >> NF4DQ_CFG_WG_SHIFT_BIT) & 0xF);
-    const int wpg = wpg_log ? (1 << wpg_log) : 4;
-    const bool tuned = U != 4 || ntl || wpg != 4 || !cfg.nontemporal;
-    if (tuned && (mode != kRef || dtype == NF4DQ_F32)) return NF4DQ_ERR_ARG;
-    const uint32_t lb = dtype == NF4DQ_F32 ? 2u : 4u;
-    const uint32_t tb = 64u * lb * U;
+    const uint32_t tb = 64u * (dtype == NF4DQ_F32 ? 2u : 4u) * kU;
     Batch<MAXB> b = bt;
     uint32_t acc = 0;
     for (uint32_t i = 0; i < b.count; ++i) {
@@ -552,93 +446,27 @@ int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_laun
     }
     b.total_tiles = acc;
     if (acc == 0) return NF4DQ_OK;
-    uint64_t blocks = (acc + wpg - 1) / wpg;
+    uint64_t blocks = (acc + kWaves - 1) / kWaves;
     if (cfg.blocks_per_cu > 0) {
         const uint64_t cap = (uint64_t)cfg.blocks_per_cu * (uint64_t)cu_count();
         if (blocks > cap) blocks = cap;
     }
-    const uint32_t sshift = (uint32_t)((cfg.flags >> NF4DQ_CFG_SEG_SHIFT_BIT) & 0xF);
-    b.seg_shift = sshift;
-    const uint64_t S = uint64_t(1) << sshift;
-    blocks = (blocks + S - 1) / S * S;  // every segment gets the same number of blocks
-
 #if NF4_FLAT_STAMPS
     b.stamps = g_stamps;
 #endif
-    const uint32_t pol = (uint32_t)((cfg.flags >> NF4DQ_CFG_STORE_POLICY_BIT) & 0xF);
-    if ((cfg.flags & (NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_X4_LOADS)) && (mode != kRef || dtype == NF4DQ_F32))
-        return NF4DQ_ERR_ARG;  // the 16 B/lane shapes: reference semantics, 16-bit outputs
-    if (cfg.flags & NF4DQ_CFG_A1_AHEAD) {  // absmax bytes a tile ahead: base shape, reference semantics
-        if (U != 4 || wpg != 4 || !cfg.nontemporal || pol || ntl || mode != kRef ||
-            (cfg.flags & (NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT)))
-            return NF4DQ_ERR_ARG;
-        if (dtype == NF4DQ_BF16) launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, 0, 4, MAXB, 0, 1>(b, blocks, st);
-        else if (dtype == NF4DQ_F16) launch_one<NF4DQ_F16, kRef, 4, kAuxStore, 0, 4, MAXB, 0, 1>(b, blocks, st);
-        else launch_one<NF4DQ_F32, kRef, 4, kAuxStore, 0, 4, MAXB, 0, 1>(b, blocks, st);
-        return hip_rc(hipGetLastError());
-    }
-    if (cfg.flags & NF4DQ_CFG_X4_DIRECT) {  // 16 B/lane loads, strided 16 B stores: base shape only
-        if (U != 4 || wpg != 4 || !cfg.nontemporal || pol || (cfg.flags & NF4DQ_CFG_X4_LOADS)) return NF4DQ_ERR_ARG;
-        if (dtype == NF4DQ_BF16) {
-            if (ntl) launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, kAuxNt, 4, MAXB, 2>(b, blocks, st);
-            else launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, 0, 4, MAXB, 2>(b, blocks, st);
-        } else {
-            if (ntl) launch_one<NF4DQ_F16, kRef, 4, kAuxStore, kAuxNt, 4, MAXB, 2>(b, blocks, st);
-            else launch_one<NF4DQ_F16, kRef, 4, kAuxStore, 0, 4, MAXB, 2>(b, blocks, st);
-        }
-        return hip_rc(hipGetLastError());
-    }
-    if (cfg.flags & NF4DQ_CFG_X4_LOADS) {  // 16 B/lane loads + LDS redistribution: base shape only
-        if (U != 4 || wpg != 4 || !cfg.nontemporal || pol) return NF4DQ_ERR_ARG;
-        if (dtype == NF4DQ_BF16) {
-            if (ntl) launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, kAuxNt, 4, MAXB, 1>(b, blocks, st);
-            else launch_one<NF4DQ_BF16, kRef, 4, kAuxStore, 0, 4, MAXB, 1>(b, blocks, st);
-        } else {
-            if (ntl) launch_one<NF4DQ_F16, kRef, 4, kAuxStore, kAuxNt, 4, MAXB, 1>(b, blocks, st);
-            else launch_one<NF4DQ_F16, kRef, 4, kAuxStore, 0, 4, MAXB, 1>(b, blocks, st);
-        }
-        return hip_rc(hipGetLastError());
-    }
-    if (pol) {  // store cache-policy experiments: base shape, reference semantics, fp16/bf16
-        if (U != 4 || ntl || wpg != 4 || !cfg.nontemporal) return NF4DQ_ERR_ARG;
-#define NF4_P(A_)                                                                         \
-    do {                                                                                  \
-        if (dtype == NF4DQ_BF16) launch_one<NF4DQ_BF16, kRef, 4, A_, 0, 4, MAXB>(b, blocks, st); \
-        else launch_one<NF4DQ_F16, kRef, 4, A_, 0, 4, MAXB>(b, blocks, st);                \
+#define NF4_D(DT_)                                                              \
+    do {                                                                        \
+        switch (mode) {                                                         \
+            case kRef: launch_one<DT_, kRef, MAXB>(b, blocks, st); break;       \
+            case kSingle: launch_one<DT_, kSingle, MAXB>(b, blocks, st); break; \
+            case kBnb: launch_one<DT_, kBnb, MAXB>(b, blocks, st); break;       \
+            default: launch_one<DT_, kBnbSingle, MAXB>(b, blocks, st); break;   \
+        }                                                                       \
     } while (0)
-        switch (pol) {
-            case 1: NF4_P(2); break;   // nt only
-            case 2: NF4_P(3); break;   // sc0 nt
-            case 3: NF4_P(19); break;  // sc0 sc1 nt
-            case 4: NF4_P(16); break;  // sc1
-            default: NF4_P(17); break; // sc0 sc1
-        }
-#undef NF4_P
-        return hip_rc(hipGetLastError());
-    }
-    if (tuned && !cfg.nontemporal) {
-        if (dtype == NF4DQ_BF16) launch_one<NF4DQ_BF16, kRef, 4, 0, 0, 4, MAXB>(b, blocks, st);
-        else launch_one<NF4DQ_F16, kRef, 4, 0, 0, 4, MAXB>(b, blocks, st);
-        if (U != 4 || ntl || wpg != 4) return NF4DQ_ERR_ARG;  // default-policy stores: base shape only
-    } else if (tuned) {
-        if (U < 4 && (ntl || (wpg != 4 && wpg != 8))) return NF4DQ_ERR_ARG;
-        if (dtype == NF4DQ_BF16) launch_tuned<NF4DQ_BF16>(b, blocks, U, ntl, wpg, st);
-        else launch_tuned<NF4DQ_F16>(b, blocks, U, ntl, wpg, st);
-    } else {
-#define NF4_D(DT_)                                                                                    \
-    do {                                                                                              \
-        switch (mode) {                                                                               \
-            case kRef: launch_one<DT_, kRef, 4, kAuxStore, 0, 4, MAXB>(b, blocks, st); break;            \
-            case kSingle: launch_one<DT_, kSingle, 4, kAuxStore, 0, 4, MAXB>(b, blocks, st); break;      \
-            case kBnb: launch_one<DT_, kBnb, 4, kAuxStore, 0, 4, MAXB>(b, blocks, st); break;            \
-            default: launch_one<DT_, kBnbSingle, 4, kAuxStore, 0, 4, MAXB>(b, blocks, st); break;        \
-        }                                                                                             \
-    } while (0)
-        if (dtype == NF4DQ_BF16) NF4_D(NF4DQ_BF16);
-        else if (dtype == NF4DQ_F16) NF4_D(NF4DQ_F16);
-        else NF4_D(NF4DQ_F32);
+    if (dtype == NF4DQ_BF16) NF4_D(NF4DQ_BF16);
+    else if (dtype == NF4DQ_F16) NF4_D(NF4DQ_F16);
+    else NF4_D(NF4DQ_F32);
 #undef NF4_D
-    }
     return hip_rc(hipGetLastError());
 }
 
@@ -783,19 +611,8 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len, const uint8_t
                         const float* absmax2, int64_t n2, void* out, int32_t out_dtype, int64_t m, int64_t n,
                         const nf4_launch_cfg* cfg, void* hip_stream) {
     nf4_launch_cfg c = cfg ? *cfg : kDefaultCfg;
-    if (c.tile_dwords != 1 && c.tile_dwords != 2 && c.tile_dwords != 4 && c.tile_dwords != 8) return NF4DQ_ERR_ARG;
-    if (c.tile_dwords < 4 && (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_A1_AHEAD |
-                                NF4DQ_CFG_STORE_POLICY_MASK)))
-        return NF4DQ_ERR_ARG;
-    if (c.flags & ~(NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_X4_LOADS | NF4DQ_CFG_X4_DIRECT | NF4DQ_CFG_A1_AHEAD | NF4DQ_CFG_SEG_SHIFT_MASK | NF4DQ_CFG_WG_SHIFT_MASK |
-                    NF4DQ_CFG_STORE_POLICY_MASK))
-        return NF4DQ_ERR_ARG;
-    if (((c.flags >> NF4DQ_CFG_SEG_SHIFT_BIT) & 0xF) > 6) return NF4DQ_ERR_ARG;
-    if (((c.flags >> NF4DQ_CFG_WG_SHIFT_BIT) & 0xF) > 4) return NF4DQ_ERR_ARG;
-    if (((c.flags >> NF4DQ_CFG_STORE_POLICY_BIT) & 0xF) > 5) return NF4DQ_ERR_ARG;
-    if (!c.nontemporal && (c.tile_dwords != 4 || (c.flags & (NF4DQ_CFG_NT_LOADS | NF4DQ_CFG_WG_SHIFT_MASK |
-                                                             NF4DQ_CFG_A1_AHEAD | NF4DQ_CFG_X4_DIRECT))))
-        return NF4DQ_ERR_ARG;
+    if (c.tile_dwords != 4 || c.nontemporal != 1 || c.blocks_per_cu < 0) return NF4DQ_ERR_ARG;
+    if (c.flags != 0) return NF4DQ_ERR_ARG;  // reserved
     return ref_impl(packed, packed_len, absmax_q, nb, absmax2, n2, out, out_dtype, m, n, c,
                     reinterpret_cast<hipStream_t>(hip_stream));
 }

@@ -36,69 +36,135 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kAuxSc1 = 16;  // write-through stores / L2-bypassing loads (cross-XCD hand-off)
 constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads return 0, stores drop
 
-// Diagnostic builds of the shared-activation kernel (tools/Makefile xsdbg): 1 = no
-// LUT reads in the dequant, 2 = no x fragment reads from LDS.
-#ifndef NF4_XS_DEBUG
-#define NF4_XS_DEBUG 0
-#endif
-// Diagnostic builds of the register-resident kernel (tools/Makefile xrdbg): 1 = no
-// per-strip LDS reduction (no barrier), 2 = no scale gathers, 3 = no dequant / MFMA,
-// 4 = 256-deep chunks through the 16-entry code table instead of the pair table.
-#ifndef NF4_XR_DEBUG
-#define NF4_XR_DEBUG 0
+// Phase-stamp hooks: empty in the library.  tools/gemm_stamps.hip defines them
+// (per-wave s_memrealtime stamps into a buffer of its own) and includes this file
+// to build the diagnostic library tools/_build/libnf4dq_gstamps.so; nothing in
+// the product reads or writes a stamp.
+//   NF4_GSTAMP(slot)          the wave's time at this point
+//   NF4_GSPAN_BEGIN()         start of a repeated span (e.g. one reduction barrier)
+//   NF4_GSPAN_END(slot)       add the span's length to slot
+#ifndef NF4_GSTAMP
+#define NF4_GSTAMP(slot_) ((void)0)
+#define NF4_GSPAN_BEGIN() ((void)0)
+#define NF4_GSPAN_END(slot_) ((void)0)
+#define NF4_GSTAMP_INIT(waves_) ((void)0)
 #endif
 
+// Split-K hand-off, in the HIP memory model with relaxed agent-scope atomics
+// only (no fence, no cache-policy assumption).  A slab entry is one 64-bit word
+// holding the fp32 partials of two adjacent columns (c, c + 1; c even), each as
+// the bitwise NOT of its bits: 0 = empty (the zero-filled workspace's state),
+// both halves nonzero = written.  Each K slice stores its partials with atomic
+// stores, then one lane draws a ticket on the strip's counter (atomic add); the
+// slice drawing ksplit - 1 resets the counter and reduces: it reads every slice's
+// entries with atomic loads, waiting per entry until it is written (per-location
+// coherence: it sees the store once it is made; the entry held 0 since the
+// previous call's reader cleared it, ordered by the kernel boundary), sums them
+// in slice order (bitwise reproducible) and clears them for the next call.  The
+// reader waits only on slices that already drew their tickets, i.e. are running
+// or done, so the wait ends; it is bounded anyway (kSpinMax polls, then NaN: a
+// wrong result, never a hung GPU -- also the outcome, correctly, of a partial that
+// is the one NaN whose NOT is 0).
+constexpr int kSpinMax = 1 << 16;
+
+__device__ __forceinline__ void slab_put2(uint64_t* slab, uint32_t e, float lo, float hi) {
+    const uint64_t w = ((uint64_t)~__float_as_uint(hi) << 32) | (uint64_t)~__float_as_uint(lo);
+    __hip_atomic_store(slab + e, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool slab_full(uint64_t w) { return (uint32_t)w != 0u && (uint32_t)(w >> 32) != 0u; }
+
+// Entry of (slice ks, row m, column pair of c) in a slab of ncols columns.
+__device__ __forceinline__ uint32_t slab_entry(uint32_t ks, uint32_t M, uint32_t m, uint32_t ncols, uint32_t c) {
+    return (ks * M + m) * (ncols >> 1) + (c >> 1);
+}
+
+// One lane's partial of column `col`, where lanes l and l ^ 1 hold columns col and
+// col ^ 1 of the same row: the even-column lane stores the pair.  All lanes call it.
+__device__ __forceinline__ void slab_put_lane(uint64_t* slab, uint32_t e, float v, uint32_t col, bool valid) {
+    const float nb = __shfl_xor(v, 1, 64);
+    if (valid && !(col & 1u)) slab_put2(slab, e, v, nb);
+}
+
+__device__ __forceinline__ bool splitk_ticket(uint32_t* ctr, uint32_t ksplit) {
+    const uint32_t t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t != ksplit - 1u) return false;
+    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
 
 // The last arriver's split-K sum for one column group of KCOLS columns: slab
-// [ksplit][M][ld] fp32 (sc1-written by every slice), columns col0.. of the
-// slab -> y[m][ycol0 ..] (row stride yld), slices added in slice order (bitwise
-// reproducible).  One wave; every lane owns float4 pieces of the group, and
-// 8 pieces x 4 slices of loads are in flight before any add -- the loads come
-// from another XCD's write-through traffic (L2-missing, ~1-2 us each), so a
-// loop that waits per element would serialise M x KCOLS / 64 of them.
+// [ksplit][M][ncols / 2] entries, columns col0.. -> y[m][ycol0 ..] (row stride yld).
+// One wave; every lane owns kU entries (column pairs) of the group, and kU x kK
+// loads are in flight before any wait -- they come from other XCDs' stores
+// (L2-missing), so waiting per entry would serialise them.
 template <int DT, uint32_t KCOLS>
-__device__ __forceinline__ void splitk_reduce(__amdgpu_buffer_rsrc_t rs, uint32_t ksplit, uint32_t M, uint32_t ld,
+__device__ __forceinline__ void splitk_reduce(uint64_t* slab, uint32_t ksplit, uint32_t M, uint32_t ncols,
                                               uint32_t col0, void* y, uint32_t yld, uint32_t ycol0, uint32_t lane) {
-    constexpr uint32_t kQ = KCOLS / 4;  // float4 pieces per row
-    constexpr int kU = 8, kK = 4;
-    const uint32_t total = M * kQ;
+    constexpr uint32_t KP = KCOLS / 2;  // entries per row of the group
+    constexpr int kU = 4, kK = 4;
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    const uint32_t total = M * KP;
+    const uint32_t sstride = M * (ncols >> 1);  // entries per slice
     for (uint32_t base = 0; base < total; base += 64u * kU) {
-        f32x4 sum[kU];
-        uint32_t off[kU];
+        float s0[kU], s1[kU];
+        uint32_t idx[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const uint32_t q = base + lane + 64u * u;
-            const uint32_t m = q / kQ, c = q % kQ;
-            off[u] = q < total ? (m * ld + col0 + 4u * c) * 4u : kOob;
+            const uint32_t e = base + lane + 64u * u;
+            idx[u] = e < total ? slab_entry(0, M, e / KP, ncols, col0 + 2u * (e % KP)) : kNone;
+            s0[u] = s1[u] = 0.0f;
         }
         for (uint32_t k0 = 0; k0 < ksplit; k0 += kK) {
-            f32x4 v[kK][kU];
+            uint64_t v[kK][kU];
+            bool ok = true;
 #pragma unroll
             for (int j = 0; j < kK; ++j)
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
-                    const uint32_t k = k0 + j;
-                    const uint32_t o = k < ksplit && off[u] != kOob ? off[u] + k * M * ld * 4u : kOob;
-                    v[j][u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, kAuxSc1));
+                    const bool live = k0 + j < ksplit && idx[u] != kNone;
+                    v[j][u] = live ? __hip_atomic_load(slab + (k0 + j) * sstride + idx[u], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : ~0ull;
+                    ok = ok && slab_full(v[j][u]);
                 }
+            if (!__all(ok)) {  // rare: an entry not written yet -- poll it
+#pragma unroll
+                for (int j = 0; j < kK; ++j)
+#pragma unroll
+                    for (int u = 0; u < kU; ++u) {
+                        uint64_t* ep = slab + (k0 + j) * sstride + idx[u];
+                        for (int tries = 0; !slab_full(v[j][u]) && tries < kSpinMax; ++tries) {
+                            __builtin_amdgcn_s_sleep(1);
+                            v[j][u] = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                        if (!slab_full(v[j][u])) v[j][u] = 0x803FFFFF803FFFFFull;  // NOT of two NaNs
+                    }
+            }
 #pragma unroll
             for (int j = 0; j < kK; ++j) {
                 if (k0 + j >= ksplit) break;  // uniform
 #pragma unroll
-                for (int u = 0; u < kU; ++u) sum[u] = (k0 + j == 0) ? v[j][u] : sum[u] + v[j][u];
+                for (int u = 0; u < kU; ++u) {
+                    const float f0 = __uint_as_float(~(uint32_t)v[j][u]);
+                    const float f1 = __uint_as_float(~(uint32_t)(v[j][u] >> 32));
+                    s0[u] = (k0 + j == 0) ? f0 : s0[u] + f0;
+                    s1[u] = (k0 + j == 0) ? f1 : s1[u] + f1;
+                    if (idx[u] != kNone)  // empty again for the next call
+                        __hip_atomic_store(slab + (k0 + j) * sstride + idx[u], 0ull, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const uint32_t q = base + lane + 64u * u;
-            if (q < total) {
-                const uint32_t m = q / kQ, c = q % kQ;
-                uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(y) + m * yld + ycol0 + 4u * c);
-                dst[0] = pack2<DT>(sum[u][0], sum[u][1]);
-                dst[1] = pack2<DT>(sum[u][2], sum[u][3]);
+            const uint32_t e = base + lane + 64u * u;
+            if (e < total) {
+                uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(y) + (e / KP) * yld + ycol0 +
+                                                            2u * (e % KP));
+                *dst = pack2<DT>(s0[u], s1[u]);
             }
         }
     }
@@ -132,7 +198,7 @@ struct GemmArgs {
     K128Mat mat[kK128GroupMax];
     uint32_t nmat;
     const void* x;          // [M][K] fp16/bf16
-    float* slab;            // [ksplit][M][ncols] fp32 partials (ksplit > 1)
+    uint64_t* slab;         // [ksplit][M][ncols] tagged fp32 partials (ksplit > 1; splitk_reduce)
     uint32_t* counters;     // one split-K ticket per column group, 0 between calls
     uint32_t M, K;
     uint32_t ncols;         // sum of N
@@ -326,14 +392,10 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
         return;
     }
 
-    // Split-K, reduced inside the launch (MI355X_MICROARCH.md / cdna guide G16,
-    // write-through form): every slice writes its fp32 partials with sc1
-    // stores, drains them, and one lane per workgroup takes a ticket on the
-    // column group's counter; the workgroup drawing ksplit-1 sums all slices
-    // in slice order (sc1 loads: no stale line from any L2), writes y, and
-    // resets the counter to 0 for the next call.  Bitwise reproducible.
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)A.slab, 0, A.ksplit * A.M * A.ncols * 4u, kRsrcFlags);
+    // Split-K, reduced inside the launch: every slice writes its fp32 partials,
+    // drains them, and one lane takes a ticket on the column group's counter
+    // (splitk_ticket / splitk_reduce); the workgroup drawing ksplit-1 sums all
+    // slices in slice order and writes y.  Bitwise reproducible.
     const uint32_t scol = Mt.col_begin + row;  // slab column of this lane (strip 0)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -342,22 +404,15 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint32_t m = 16u * mt + 4u * kh + r;
-                const uint32_t off = m < A.M ? ((ks * A.M + m) * A.ncols + scol + 16u * nt) * 4u : 0xFFFFFFF0u;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][nt][r]), rs, off, 0, kAuxSc1);
+                slab_put_lane(A.slab, slab_entry(ks, A.M, m, A.ncols, scol + 16u * nt), acc[mt][nt][r], scol, m < A.M);
             }
         }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // only wave 0 is left: its own drain is the hand-off
     uint32_t last = 0;
-    if (lane == 0) {
-        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[cg], 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        last = ticket == A.ksplit - 1u;
-        if (last) __hip_atomic_store(&A.counters[cg], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (lane == 0) last = splitk_ticket(&A.counters[cg], A.ksplit);
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
-    splitk_reduce<DT, 16u * NT>(rs, A.ksplit, A.M, A.ncols, Mt.col_begin + cgl * 16u * NT, Mt.y, Mt.N, cgl * 16u * NT,
-                                lane);
+    splitk_reduce<DT, 16u * NT>(A.slab, A.ksplit, A.M, A.ncols, Mt.col_begin + cgl * 16u * NT, Mt.y, Mt.N,
+                                cgl * 16u * NT, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -470,26 +525,10 @@ __global__ __launch_bounds__(64 * WV, 4) void nf4_gemm_xs_kernel(const GemmArgs 
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
-#if NF4_XS_DEBUG == 2
-                    ch.x[mt][s] = u32x4{(uint32_t)j, nl, kh, (uint32_t)s};  // diagnostic: no x reads
-#else
                     ch.x[mt][s] = *reinterpret_cast<const u32x4*>(smem + (16u * mt + nl) * XS + (uint32_t)j * 256u +
                                                                  64u * kh + 16u * s);
-#endif
             const float scs[1] = {scl[srow + 2u * (uint32_t)j]};
-#if NF4_XS_DEBUG == 1
-            // diagnostic: no LUT reads (the weight bits go straight into the MMA)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) {
-                    const u32x4 bw = {ch.w[0][s4], ch.w[0][s4] ^ __float_as_uint(scs[0]), ch.w[0][s4] >> 1, ch.w[0][s4] << 1};
-                    acc[mt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        __builtin_bit_cast(bf16x8, ch.x[mt][s4]), __builtin_bit_cast(bf16x8, bw), acc[mt][0], 0, 0, 0);
-                }
-#else
             chunk_mma<DT, MT, 1>(ch, lut, scs, acc);
-#endif
         }
     }
     if (!live) return;
@@ -505,31 +544,22 @@ __global__ __launch_bounds__(64 * WV, 4) void nf4_gemm_xs_kernel(const GemmArgs 
             }
         return;
     }
-    // split-K: this wave's strip slice to the slab (write-through), drained; one
-    // ticket per strip; the last arriver sums the slices in slice order
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)A.slab, 0, A.ksplit * A.M * A.ncols * 4u, kRsrcFlags);
+    // split-K: this wave's strip slice to the slab; one ticket per strip; the last
+    // arriver sums the slices in slice order (splitk_ticket / splitk_reduce)
     const uint32_t scol = Mt.col_begin + row;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t m = 16u * mt + 4u * kh + r;
-            const uint32_t off = m < A.M ? ((ks * A.M + m) * A.ncols + scol) * 4u : kOob;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][0][r]), rs, off, 0, kAuxSc1);
+            slab_put_lane(A.slab, slab_entry(ks, A.M, m, A.ncols, scol), acc[mt][0][r], scol, m < A.M);
         }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partials are out: the hand-off
     const uint32_t ctr = (Mt.col_begin >> 4) + strip;
     uint32_t last = 0;
-    if (lane == 0) {
-        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[ctr], 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        last = ticket == A.ksplit - 1u;
-        if (last) __hip_atomic_store(&A.counters[ctr], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (lane == 0) last = splitk_ticket(&A.counters[ctr], A.ksplit);
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
-    splitk_reduce<DT, 16u>(rs, A.ksplit, A.M, A.ncols, Mt.col_begin + strip * 16u, Mt.y, Mt.N, strip * 16u, lane);
+    splitk_reduce<DT, 16u>(A.slab, A.ksplit, A.M, A.ncols, Mt.col_begin + strip * 16u, Mt.y, Mt.N, strip * 16u, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -627,16 +657,9 @@ __device__ __forceinline__ void xslot_issue(const GemmArgs& A, uint32_t strip, b
 #pragma unroll
         for (int q = 0; q < WQ; ++q)
             s.w[WQ * h + q] = __builtin_amdgcn_raw_buffer_load_b128(rw, (w0 + 16u * q) | oob, 0, 0);
-#if NF4_XR_DEBUG == 2
-        s.qa[h] = (uint8_t)(fmodu(r0 * A.bpr + 2u * c + ln.b1, Mt.nb) | 1u);
-        s.qb[h] = __uint_as_float(0x3c000000u | (fmodu(r0 * A.groups + (c >> 1) + ln.b2, Mt.n2) & 0xFFu));
-        (void)ra1;
-        (void)ra2;
-#else
         s.qa[h] = __builtin_amdgcn_raw_buffer_load_b8(ra1, fmodu(r0 * A.bpr + 2u * c + ln.b1, Mt.nb) | oob, 0, 0);  // (:173-177)
         s.qb[h] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
             ra2, (fmodu(r0 * A.groups + (c >> 1) + ln.b2, Mt.n2) * 4u) | oob, 0, 0));  // (:40-41, :183-186)
-#endif
     }
 }
 
@@ -722,6 +745,8 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     const uint32_t cw = (ks * (uint32_t)WV + wave) * (uint32_t)KPW;  // the wave's first chunk
     const XLane ln{nl * (A.K >> 1) + (KPW >= 2 ? 32u : 16u) * kh, nl * A.bpr + (KPW >= 2 ? kh : kh >> 1),
                    nl * A.groups};
+    NF4_GSTAMP_INIT(WV);
+    NF4_GSTAMP(0);
 
     // 1. the wave's x fragments (rows >= M and chunks past K read as zeros),
     //    then the ring's first D strips, then the code table
@@ -761,6 +786,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     }
     const uint32_t slot8 = (lane & 31u) * 8u;
     __syncthreads();
+    NF4_GSTAMP(1);
 
     // 2. the strips: dequant + MFMA of the wave's chunks, partial tile to LDS,
     //    one barrier, the tile's reducer wave sums the WV partials in wave order
@@ -777,7 +803,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
             if (live) {
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if constexpr (KPW >= 2 && NF4_XR_DEBUG != 4) {
+                if constexpr (KPW >= 2) {
 #pragma unroll
                     for (int h = 0; h < KPW / 2; ++h) {
                         const u32x4 (&xs)[2][MT][4] = *reinterpret_cast<const u32x4 (*)[2][MT][4]>(&xf[2 * h]);
@@ -785,8 +811,9 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
                                             qtab[ring[d].qa[h]] * ring[d].qb[h], ptab, slot8, xs, acc);
                     }
                 }
+                if (t == 0) NF4_GSTAMP(2);  // x and the first strip's weights arrived, first strip done
 #pragma unroll
-                for (int q = 0; q < (KPW >= 2 && NF4_XR_DEBUG != 4 ? 0 : KPW); ++q) {
+                for (int q = 0; q < (KPW >= 2 ? 0 : KPW); ++q) {
                     Chunk<MT, 1> ch;
                     ch.w[0] = ring[d].w[q];
 #pragma unroll
@@ -797,11 +824,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
                     f32x4 a1[MT][1];
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) a1[mt][0] = acc[mt];
-#if NF4_XR_DEBUG == 3
-                    a1[0][0][q & 3] += __uint_as_float((ch.w[0][0] ^ ch.w[0][1] ^ ch.w[0][2] ^ ch.w[0][3]) & 0x3fffffffu) * scs[0];
-#else
                     chunk_mma<DT, MT, 1>(ch, lut, scs, a1);
-#endif
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) acc[mt] = a1[mt][0];
                 }
@@ -811,20 +834,8 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
             __builtin_amdgcn_sched_barrier(0);
             if (d % R != R - 1) continue;  // the group's partials meet after its last strip
             const uint32_t tg = t + 1u - (uint32_t)R;  // first strip of the group
-#if NF4_XR_DEBUG == 1
-            if (tg < nst && wave == 0) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (tg + r >= nst) break;
-                    float* h = held + (tg + r) * (16u * MT * 16u) + 4u * kh * 16u + nl;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) h[16u * q] = accs[r][0][q];
-                }
-            }
-            if (false) {
-#else
             if (tg < nst) {  // uniform
-#endif
+                NF4_GSPAN_BEGIN();
                 // red slot of strip u: ((u / R) & 1) * R + u % R (two groups in flight)
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
@@ -836,6 +847,8 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
                     }
                 }
                 __syncthreads();
+                NF4_GSPAN_END(7);  // partial tiles stored + the barrier
+                NF4_GSPAN_BEGIN();
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t u = tg + (uint32_t)r;
@@ -853,10 +866,13 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
                         }
                     }
                 }
+                NF4_GSPAN_END(8);  // the reducer's sums
             }
         }
     }
+    NF4_GSTAMP(3);
     __syncthreads();
+    NF4_GSTAMP(4);
 
     // 3. the results: straight to y (one slice), or to the slab + tickets
     const uint32_t rows = A.M;
@@ -871,35 +887,29 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
                                                         (strip - Mt.cg_begin) * 16u + 2u * p);
             *dst = pack2<DT>(h[0], h[1]);
         }
+        NF4_GSTAMP(5);
         return;
     }
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)A.slab, 0, A.ksplit * A.M * A.ncols * 4u, kRsrcFlags);
-    // slab [ks][M][ncols] fp32 (strip s at columns 16 s), write-through, drained
-    for (uint32_t e = tid; e < nst * rows * 4u; e += 64u * WV) {
-        const uint32_t t = e / (rows * 4u), rem = e - t * rows * 4u, m = rem >> 2, p = rem & 3u;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(held + t * (16u * MT * 16u) + m * 16u + 4u * p);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs,
-                                               ((ks * A.M + m) * A.ncols + (s0 + t) * 16u + 4u * p) * 4u, 0, kAuxSc1);
+    // slab [ks][M][ncols] entries (strip s at columns 16 s): splitk_ticket / splitk_reduce
+    for (uint32_t e = tid; e < nst * rows * 8u; e += 64u * WV) {  // column pairs
+        const uint32_t t = e / (rows * 8u), rem = e - t * rows * 8u, m = rem >> 3, c = 2u * (rem & 7u);
+        const float* h = held + t * (16u * MT * 16u) + m * 16u + c;
+        slab_put2(A.slab, slab_entry(ks, A.M, m, A.ncols, (s0 + t) * 16u + c), h[0], h[1]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's slab stores are out
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's entries are out before its tickets
+    NF4_GSTAMP(5);
     __syncthreads();
-    if (tid < nst) {  // one ticket per strip; nst <= 64 (host-checked)
-        const uint32_t strip = s0 + tid;
-        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[strip], 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t last = ticket == S - 1u;
-        if (last) __hip_atomic_store(&A.counters[strip], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_flags[tid] = last;
-    }
+    if (tid < nst) last_flags[tid] = splitk_ticket(&A.counters[s0 + tid], S);  // one ticket per strip; nst <= 64
     __syncthreads();
     for (uint32_t t = wave; t < nst; t += (uint32_t)WV) {
         if (!last_flags[t]) continue;  // uniform
         const uint32_t strip = s0 + t;
         const K128Mat& Mt = A.mat[xr_mat_of(A, strip)];
         const uint32_t lc = (strip - Mt.cg_begin) * 16u;
-        splitk_reduce<DT, 16u>(rs, S, A.M, A.ncols, strip * 16u, Mt.y, Mt.N, lc, lane);
+        NF4_GSTAMP(6);  // tickets drawn: this wave reduces (the last arriver)
+        splitk_reduce<DT, 16u>(A.slab, S, A.M, A.ncols, strip * 16u, Mt.y, Mt.N, lc, lane);
     }
+    NF4_GSTAMP(9);
 }
 
 // ---------------------------------------------------------------------------
@@ -939,7 +949,7 @@ struct StreamArgs {
     uint32_t sg_total;      // strip groups over all weights
     uint32_t ncols;         // sum of N (split-K slab row length)
     const void* x;
-    float* slab;
+    uint64_t* slab;
     uint32_t* counters;
     uint32_t M, K;
     uint32_t T, parts;      // strips per workgroup, K parts per strip
@@ -952,39 +962,13 @@ struct StreamArgs {
     uint32_t zero_off;      // 128 zero bytes: the A operand of rows >= M
     uint32_t red_off;       // [W][MT][64] f32x4 partial sums (persistent: two sets)
     uint32_t out_off;       // persistent: finished outputs [group][strip][M][16] (16-bit)
-    unsigned long long* stamps;  // NF4_STREAM_DEBUG == 3 only
 };
-
-#if NF4_STREAM_DEBUG == 3
-#define NF4_STAMP(slot_)                                                                              \
-    do {                                                                                              \
-        __builtin_amdgcn_sched_barrier(0);                                                            \
-        unsigned long long t_;                                                                        \
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
-        if (lane == 0) A.stamps[(blockIdx.x * W + wave) * 8u + (slot_)] = t_;                         \
-        __builtin_amdgcn_sched_barrier(0);                                                            \
-    } while (0)
-#else
-#define NF4_STAMP(slot_) \
-    do {                 \
-    } while (0)
-#endif
 
 struct SSlot {
     u32x4 w0, w1;
     uint32_t qa;
     float qb;
 };
-
-// Diagnostic builds only (tools/Makefile): 1 = loads without the dequant/MMA
-// body, 2 = the body on register-made data without weight loads, 3 = per-wave
-// s_memrealtime stamps (start, prologue done, loop done, end) into the
-// workspace after the counter region (ksplit 1 only), 4 = no absmax loads,
-// 5 = neither weight loads nor dequant, 6 = no activation loads (x staged from registers),
-// 7 = 5 without the pair-table build (stream kernel).
-#ifndef NF4_STREAM_DEBUG
-#define NF4_STREAM_DEBUG 0
-#endif
 
 constexpr int kVsMax = 16;  // chunks per wave covered by the vector-scale form  // beyond every buffer range: loads return 0, no traffic
 
@@ -997,29 +981,14 @@ __device__ __forceinline__ void sslot_issue(const StreamArgs& A, const StreamMat
     // the waitcnt pass sees one straight-line ring
     const uint32_t oob = valid ? 0u : kOob;
     const uint32_t woff = (row * (A.K >> 1) + c * 128u + kh * 32u) | oob;
-#if NF4_STREAM_DEBUG == 2 || NF4_STREAM_DEBUG == 5 || NF4_STREAM_DEBUG == 7
-    s.w0 = u32x4{woff, woff * 3u, woff ^ 0x5555u, c};
-    s.w1 = u32x4{c * 7u, woff + c, row, kh};
-    s.qa = (woff >> 3) & 0xFFu;
-    s.qb = 0.001f;
-    (void)rw; (void)ra1; (void)ra2;
-    return;
-#endif
     s.w0 = __builtin_amdgcn_raw_buffer_load_b128(rw, woff, 0, 0);
     s.w1 = __builtin_amdgcn_raw_buffer_load_b128(rw, woff + 16u, 0, 0);
     if constexpr (!VS) {
         // block 4c + kh of the row; its nested group is c (reference wraps, :173-186)
         const uint32_t i1 = fmodu(row * A.bpr + 4u * c + kh, Mt.nb) | oob;
         const uint32_t i2 = (fmodu(row * A.groups + c, Mt.n2) * 4u) | oob;
-#if NF4_STREAM_DEBUG == 4
-        s.qa = i1 & 0xFFu;
-        s.qb = __uint_as_float(i2 & 0x3FFFFFFFu);
-        (void)ra1;
-        (void)ra2;
-#else
         s.qa = __builtin_amdgcn_raw_buffer_load_b8(ra1, i1, 0, 0);
         s.qb = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra2, i2, 0, 0));
-#endif
     }
 }
 
@@ -1106,17 +1075,8 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     const uint32_t nloc = s1 - s0;
     const uint32_t l0 = part * A.cpp;  // first chunk of this wave within the slice
     const uint32_t cnt = nloc > l0 ? (nloc - l0 < A.cpp ? nloc - l0 : A.cpp) : 0u;
-    NF4_STAMP(0);
-#if NF4_STREAM_DEBUG == 3
-    if (lane == 0) {
-        uint32_t hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        A.stamps[(blockIdx.x * W + wave) * 8u + 6u] = hw;
-        A.stamps[(blockIdx.x * W + wave) * 8u + 7u] = xcc;
-    }
-#endif
+    NF4_GSTAMP_INIT(W);
+    NF4_GSTAMP(0);
 
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * (A.K >> 1), kRsrcFlags);
     const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a1, 0, Mt.nb_bytes, kRsrcFlags);
@@ -1133,12 +1093,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
         const uint32_t p = tid + (uint32_t)i * 64u * W;
         const uint32_t r = fdiv(p, A.ppr), q = p - r * A.ppr.d;
         const bool ok = p < pieces && s0 * 256u + q * 8u < A.K;
-#if NF4_STREAM_DEBUG == 6
-        xv[i] = u32x4{p, r, q, (uint32_t)ok};
-        (void)rx;
-#else
         xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? (r * A.K + s0 * 256u) * 2u + q * 16u : kOob, 0, 0);
-#endif
         xdst[i] = p < pieces ? kLdsX + r * A.xstride + q * 16u : 0xFFFFFFFFu;
     }
     // 2. the weight ring (VS: the wave's scales first)
@@ -1173,21 +1128,16 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     // (lo, t) and writes it for all 16 hi -- the hi codes are immediates.
     if (tid < 256u) qtab[tid] = (float)tid / 127.0f;  // IEEE division
     if (tid < 8u) *reinterpret_cast<u32x4*>(smem + A.zero_off + 16u * tid) = u32x4{0u, 0u, 0u, 0u};
-#if NF4_STREAM_DEBUG != 7
     for (uint32_t u = tid; u < 16u * 32u; u += 64u * W) {
         const float clo = nf4_code(u >> 5);
 #pragma unroll
         for (int hi = 0; hi < 16; ++hi) ptab[(16u * hi + (u >> 5)) * 32u + (u & 31u)] = f32x2{nf4_code(hi), clo};
     }
-#endif
 #pragma unroll
     for (int i = 0; i < XR; ++i)
         if (xdst[i] != 0xFFFFFFFFu) *reinterpret_cast<u32x4*>(smem + xdst[i]) = xv[i];
     __syncthreads();
-    NF4_STAMP(1);
-#if NF4_STREAM_DEBUG == 3
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-#endif
+    NF4_GSTAMP(1);
 
     uint32_t xa0[MT];
     bool live[MT];
@@ -1205,12 +1155,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
         uint32_t xa[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) xa[mt] = live[mt] ? xa0[mt] + l * 512u : xa0[mt];
-#if NF4_STREAM_DEBUG == 1 || NF4_STREAM_DEBUG == 4 || NF4_STREAM_DEBUG == 5 || NF4_STREAM_DEBUG == 7
-        acc[0][0] += __uint_as_float((ring[j].w0[0] ^ ring[j].w1[3] ^ qa) & 0x3FFFFFFFu) * qb;
-        (void)xa;
-#else
         sslot_mma<DT, MT>(ring[j], qa, qb, ptab, qtab, smem, slot8, xa, acc, accb);
-#endif
     };
     if constexpr (VS) {
         // fully unrolled: ring slot jj % P, scale lanes jj / 4 and jj % 4 are static
@@ -1247,7 +1192,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
 
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] += accb[mt];
-    NF4_STAMP(2);
+    NF4_GSTAMP(2);
     // 4. the strip's K parts meet in LDS, in part order (the partials reuse the
     // x slice's LDS once every wave is done reading it)
     __syncthreads();
@@ -1271,32 +1216,23 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
                 const uint32_t m = 16u * mt + 4u * kh + r;
                 if (m < A.M) store_y<DT>(Mt.y, m * Mt.N + row, acc[mt][r]);
             }
-        NF4_STAMP(3);
+        NF4_GSTAMP(3);
         return;
     }
     // 5. split-K across workgroups: the hand-off of nf4_gemm_smallm_kernel, per strip
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)A.slab, 0, A.ksplit * A.M * A.ncols * 4u, kRsrcFlags);
     const uint32_t gstrip = Mt.strip_begin + strip;  // launch-wide strip: counter and slab column
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t m = 16u * mt + 4u * kh + r;
-            const uint32_t off = m < A.M ? ((ks * A.M + m) * A.ncols + gstrip * 16u + nl) * 4u : kOob;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mt][r]), rs, off, 0, kAuxSc1);
+            slab_put_lane(A.slab, slab_entry(ks, A.M, m, A.ncols, gstrip * 16u + nl), acc[mt][r], nl, m < A.M);
         }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t last = 0;
-    if (lane == 0) {
-        const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[gstrip], 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        last = ticket == A.ksplit - 1u;
-        if (last) __hip_atomic_store(&A.counters[gstrip], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (lane == 0) last = splitk_ticket(&A.counters[gstrip], A.ksplit);
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
-    splitk_reduce<DT, 16u>(rs, A.ksplit, A.M, A.ncols, gstrip * 16u, Mt.y, Mt.N, strip * 16u, lane);
+    splitk_reduce<DT, 16u>(A.slab, A.ksplit, A.M, A.ncols, gstrip * 16u, Mt.y, Mt.N, strip * 16u, lane);
 }
 
 
@@ -1346,6 +1282,8 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     const uint32_t rounds = cnt / P, total = mine * rounds;
     const uint32_t l0 = part * cnt;          // first chunk of this wave within the slice
     const uint32_t cbase = ks * A.cps;       // first chunk of the slice within K
+    NF4_GSTAMP_INIT(W);
+    NF4_GSTAMP(0);
 
     auto geo = [&](uint32_t it, PGeo& g) {
         const uint32_t sgi = j0 + it * G;
@@ -1418,6 +1356,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     for (int i = 0; i < kXR; ++i)
         if (xdst[i] != 0xFFFFFFFFu) *reinterpret_cast<u32x4*>(smem + xdst[i]) = xv[i];
     __syncthreads();
+    NF4_GSTAMP(1);
 
     const bool live = nl < A.M;
     const uint32_t xa0 = live ? kLdsX + nl * A.xstride + kh * 128u : A.zero_off;
@@ -1435,6 +1374,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
             const uint32_t xa[1] = {live ? xa0 + l * 512u : xa0};
             sslot_mma<DT, 1>(ring[s], (cur.a1[s] >> (8u * kh)) & 0xFFu, __uint_as_float(cur.a2[s]), ptab, qtab, smem,
                              slot8, xa, acc, accb);
+            if (it == 0 && rr == 0 && s == 0) NF4_GSTAMP(2);  // first chunk's weights arrived and consumed
             __builtin_amdgcn_sched_barrier(0);
             issue_w(ring[s], s, more);
             __builtin_amdgcn_sched_barrier(0);
@@ -1442,8 +1382,10 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         advance();
         if (++rr == rounds) {  // group `it` done (uniform)
             f32x4* red = reinterpret_cast<f32x4*>(smem + A.red_off) + buf * (64u * W);
+            NF4_GSPAN_BEGIN();
             red[wave * 64u + lane] = acc[0] + accb[0];
             __syncthreads();
+            NF4_GSPAN_END(7);
             if (part == 0) {
                 f32x4 sum = red[wave * 64u + lane];
                 for (uint32_t q = 1; q < A.parts; ++q) sum += red[(wave + q * A.T) * 64u + lane];
@@ -1475,7 +1417,9 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         if (g + 1 < total) round(sc[1], sc[0]);
     }
     // 3. the workgroup's outputs
+    NF4_GSTAMP(3);
     __syncthreads();
+    NF4_GSTAMP(4);
     const uint32_t per = A.T * A.M * 16u;
     if constexpr (!SPLIT) {
         const uint16_t* o = reinterpret_cast<const uint16_t*>(smem + A.out_off);
@@ -1489,14 +1433,13 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
             const uint32_t col = ((sgi - Mt.sg_begin) * A.T + t) * 16u + (rem2 & 15u);
             reinterpret_cast<uint16_t*>(Mt.y)[(rem2 >> 4) * Mt.N + col] = o[i];
         }
+        NF4_GSTAMP(5);
     } else {
-    // 3b. K slices: the partials to the slab [ksplit][M][ncols] (write-through
-    // stores, drained), then per strip group a ticket; the slice drawing
-    // ksplit - 1 sums all slices in slice order (nf4_gemm_smallm_kernel's hand-off)
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)A.slab, 0, KS * A.M * A.ncols * 4u, kRsrcFlags);
+    // 3b. K slices: the partials to the slab [ksplit][M][ncols], then per strip
+    // group a ticket; the slice drawing ksplit - 1 sums all slices in slice order
+    // (splitk_ticket / splitk_reduce)
     const float* o32 = reinterpret_cast<const float*>(smem + A.out_off);
-    for (uint32_t i = 4u * tid; i < mine * per; i += 4u * 64u * W) {
+    for (uint32_t i = 2u * tid; i < mine * per; i += 2u * 64u * W) {  // column pairs
         const uint32_t ito = i / per, rem = i - ito * per;
         const uint32_t t = rem / (A.M * 16u), rem2 = rem - t * (A.M * 16u);
         const uint32_t sgi = j0 + ito * G;
@@ -1504,20 +1447,14 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         for (uint32_t j = 1; j < A.nmat; ++j) mi = sgi >= A.mat[j].sg_begin ? j : mi;
         const StreamMat& Mt = A.mat[mi];
         const uint32_t gstrip = Mt.strip_begin + (sgi - Mt.sg_begin) * A.T + t;
-        const uint32_t off = ((ks * A.M + (rem2 >> 4)) * A.ncols + gstrip * 16u + (rem2 & 15u)) * 4u;
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(o32 + i), rs, off, 0, kAuxSc1);
+        slab_put2(A.slab, slab_entry(ks, A.M, rem2 >> 4, A.ncols, gstrip * 16u + (rem2 & 15u)), o32[i], o32[i + 1]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's entries are out before its tickets
     __syncthreads();
     for (uint32_t ito = wave; ito < mine; ito += W) {
         const uint32_t sgi = j0 + ito * G;
         uint32_t last = 0;
-        if (lane == 0) {
-            const uint32_t ticket = __hip_atomic_fetch_add(&A.counters[sgi], 1u, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-            last = ticket == KS - 1u;
-            if (last) __hip_atomic_store(&A.counters[sgi], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (lane == 0) last = splitk_ticket(&A.counters[sgi], KS);
         last = __builtin_amdgcn_readfirstlane(last);
         if (!last) continue;
         uint32_t mi = 0;
@@ -1525,11 +1462,13 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         const StreamMat& Mt = A.mat[mi];
         const uint32_t s0 = (sgi - Mt.sg_begin) * A.T;  // first strip of the group within the weight
         const uint32_t col0 = (Mt.strip_begin + s0) * 16u;
-        if (A.T == 4) splitk_reduce<DT, 64u>(rs, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
-        else if (A.T == 2) splitk_reduce<DT, 32u>(rs, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
-        else splitk_reduce<DT, 16u>(rs, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
+        if (A.T == 4) splitk_reduce<DT, 64u>(A.slab, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
+        else if (A.T == 2) splitk_reduce<DT, 32u>(A.slab, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
+        else splitk_reduce<DT, 16u>(A.slab, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
     }
+    NF4_GSTAMP(5);
     }
+    NF4_GSTAMP(9);
 }
 
 // ---- decomposition choice --------------------------------------------------
@@ -1709,7 +1648,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 inline int hip_rc2(hipError_t e) { return e == hipSuccess ? NF4DQ_OK : NF4DQ_ERR_HIP_BASE + (int)e; }
 
-// Workspace: [64 KiB of uint32 ticket counters][ksplit * M * N fp32 partials].
+// Workspace: [64 KiB of uint32 ticket counters][ksplit * M * N / 2 64-bit slab entries].
 // The counter region has a fixed size so that no call's partials ever overlay
 // another call's counters (those must stay 0 between calls): N <= 2^18.
 constexpr size_t kCounterBytes = 64 * 1024;
@@ -1717,7 +1656,7 @@ static size_t counters_bytes(int64_t) { return kCounterBytes; }
 
 static size_t workspace_for(int64_t M, int64_t N, int64_t K, const nf4_gemm_cfg& c) {
     if (M <= 0 || N <= 0 || K <= 0 || N % 64 || K % kChunkK) return 0;
-    return c.ksplit > 1 ? counters_bytes(N) + (size_t)c.ksplit * (size_t)M * (size_t)N * sizeof(float) : 0;
+    return c.ksplit > 1 ? counters_bytes(N) + (size_t)c.ksplit * (size_t)M * (size_t)N * 4u : 0;  // 8-B entry per 2 columns
 }
 
 static int device_cus() {
@@ -1744,7 +1683,7 @@ struct HostMat {
 };
 
 // One launch of the streaming kernel over `count` weights sharing x (shapes and
-// cfg already validated; workspace = counters + ksplit * M * sum(N) fp32).
+// cfg already validated; workspace = counters + ksplit * M * sum(N) / 2 64-bit slab entries).
 static int launch_stream(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
                          const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st) {
     const StreamPlan pl = stream_plan(M, K, cfg);
@@ -1753,7 +1692,7 @@ static int launch_stream(const HostMat* mats, int count, const void* x, int64_t 
     S.nmat = (uint32_t)count;
     S.x = x;
     S.counters = reinterpret_cast<uint32_t*>(workspace);
-    S.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    S.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
     S.M = (uint32_t)M;
     S.K = (uint32_t)K;
     S.T = (uint32_t)cfg.strips;
@@ -1768,9 +1707,6 @@ static int launch_stream(const HostMat* mats, int count, const void* x, int64_t 
     S.xstride = pl.xstride;
     S.zero_off = pl.zero_off;
     S.red_off = pl.red_off;
-#if NF4_STREAM_DEBUG == 3
-    S.stamps = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + kCounterBytes);
-#endif
     // vector scales: no absmax wrap inside any row of any weight, and each wave's chunks <= kVsMax
     bool vs = S.cpp <= (uint32_t)kVsMax;
     uint32_t sg = 0, strips = 0;
@@ -1849,7 +1785,7 @@ static int launch_persist(const HostMat* mats, int count, const void* x, int64_t
     S.nmat = (uint32_t)count;
     S.x = x;
     S.counters = reinterpret_cast<uint32_t*>(workspace);
-    S.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    S.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
     S.M = (uint32_t)M;
     S.K = (uint32_t)K;
     S.T = (uint32_t)cfg.strips;
@@ -1938,7 +1874,7 @@ static int launch_persist(const HostMat* mats, int count, const void* x, int64_t
 }
 
 // One launch of the 128-deep kernel over `count` weights sharing x (shapes and
-// cfg validated; workspace = counters + ksplit * M * sum(N) fp32 when ksplit > 1).
+// cfg validated; workspace = counters + ksplit * M * sum(N) / 2 64-bit slab entries when ksplit > 1).
 // LDS bytes of the shared-activation kernel: x slice (16 MT rows) + scale table + LUT.
 static uint32_t xs_lds_bytes(int64_t M, int kc, int waves) {
     const uint32_t mt = M > 16 ? 2u : 1u;
@@ -1954,7 +1890,7 @@ static int launch_xs(const HostMat* mats, int count, const void* x, int64_t M, i
     A.nmat = (uint32_t)count;
     A.x = x;
     A.counters = reinterpret_cast<uint32_t*>(workspace);
-    A.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    A.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
     A.M = (uint32_t)M;
     A.K = (uint32_t)K;
     A.ksplit = ks;
@@ -2044,7 +1980,7 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
     A.nmat = (uint32_t)count;
     A.x = x;
     A.counters = reinterpret_cast<uint32_t*>(workspace);
-    A.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    A.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
     A.M = (uint32_t)M;
     A.K = (uint32_t)K;
     A.ksplit = ks;
@@ -2122,7 +2058,7 @@ static int launch_k128(const HostMat* mats, int count, const void* x, int64_t M,
     A.nmat = (uint32_t)count;
     A.x = x;
     A.counters = reinterpret_cast<uint32_t*>(workspace);
-    A.slab = ks > 1 ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    A.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
     A.M = (uint32_t)M;
     A.K = (uint32_t)K;
     A.ksplit = ks;

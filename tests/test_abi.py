@@ -110,7 +110,9 @@ def test_cfg_validation():
     L = _lib.lib()
     cfg = _lib.LaunchCfg(3, 0, 0, 0)
     assert L.nf4_dequant_ref_cfg(FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, ctypes.byref(cfg), None) == _lib.ERR_ARG
-    for bad in ((4, 0, 0, 8), (8, 0, 0, 0), (4, 0, 0, 1), (4, 0, 1, 0x50), (4, 0, 1, 0x700), (4, 0, 0, 0x20)):
+    # only tile_dwords 4, nontemporal 1, a grid cap >= 0 and the absmax prefetch field remain
+    for bad in ((8, 0, 1, 0), (2, 0, 1, 0), (4, 0, 0, 0), (4, -1, 1, 0), (4, 0, 1, 1), (4, 0, 1, 0x8),
+                (4, 0, 1, 0x100), (4, 0, 1, 0x2000), (4, 0, 1, 0x10000)):
         cfg = _lib.LaunchCfg(*bad)
         assert L.nf4_dequant_ref_cfg(FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, ctypes.byref(cfg), None) == \
             _lib.ERR_ARG, bad

@@ -6,7 +6,7 @@ handed -- inputs, outputs, the GEMM workspace -- is carved out of a larger
 allocation with 64 KiB guard bands of a fixed byte pattern on both sides.  After
 each call: both bands of every buffer intact (no write outside a buffer), the
 inputs unchanged (no write into an input), the output equal to the oracle, and
-the split-K ticket counters back at zero.  Shapes take ragged tails (partial
+the split-K ticket counters and slab entries back at zero.  Shapes take ragged tails (partial
 tiles, partial 64-blocks, odd n, single rows, wrapping / truncated statistics,
 strips not filling a workgroup), where range handling matters.
 (The host path has its own ASan/UBSan run: tests/test_cpu_sanitizers.py.)
@@ -203,7 +203,9 @@ def test_gemm_every_decomposition(coracle, gpu, M, N, K):
         assert y.bands_intact(), f"write outside y, cfg {what}"
         assert ws.bands_intact(), f"write outside the workspace, cfg {what}"
         if wsz:
+            # tickets back at 0 and every split-K slab entry read and cleared (empty) again
             assert int(ws.body()[:min(COUNTER_BYTES, wsz)].count_nonzero()) == 0, f"tickets not reset, cfg {what}"
+            assert int(ws.body().count_nonzero()) == 0, f"slab entries not cleared, cfg {what}"
         bad = (y.body(torch.bfloat16).view(M, N).double() - ref_t).abs() > tol_t
         assert not bool(bad.any()), (what, int(bad.sum()))
         ran += 1
@@ -236,7 +238,7 @@ def test_gemm_grouped(coracle, gpu):
     assert rc == 0, _lib.strerror(rc)
     assert ws.bands_intact()
     if wsz:
-        assert int(ws.body()[:min(COUNTER_BYTES, wsz)].count_nonzero()) == 0
+        assert int(ws.body().count_nonzero()) == 0  # tickets and slab entries back at 0
     for N, gp, ga1, ga2, y, (p, a1, a2) in keep:
         assert y.bands_intact(), f"write outside y of the {N}-column weight"
         ref, tol = _gemm_ref(coracle.dequant_ref(p, a1, a2, N, K, O.BF16), xb)

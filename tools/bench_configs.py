@@ -7,9 +7,11 @@ c3   Llama-3-8B: 32 layers x {q,o 4096x4096; k,v 1024x4096; gate,up 14336x4096;
      C ABI (nf4_dequant_ref_batched, <= NF4DQ_BATCH_MAX matrices per launch).
 c3b  the "4096/11008" shape set BASELINE names (Llama-2-7B: q,k,v,o 4096x4096;
      gate,up 11008x4096; down 4096x11008), same method.
-c4   4096x4096 NF4 -> fp16 vs bf16 vs fp32 output, single launches over 16
-     rotating buffer sets, hipGraph replay.
-c5   one 8192x8192 NF4->bf16 matrix (the per-GPU unit of the 8-GPU config).
+c4   4096x4096 NF4 -> fp16 vs bf16 vs fp32 output, single launches over rotating
+     buffer sets (13 for 16-bit output, as bench.py: >= 512 MiB), timed as bench.py times its steps
+     (eager, behind a device spin), the hipGraph replay beside it.
+c5   one 8192x8192 NF4->bf16 matrix (the per-GPU unit of the 8-GPU config), 4 sets,
+     the same method.
 big  128256x8192 NF4->bf16 (Llama-3-70B lm_head size: 525 MB packed, past one buffer
      descriptor -- two row pieces in one launch).
 bnb  4096x4096 NF4->bf16 with bitsandbytes semantics (nf4_dequant_bnb: code2[A1] * A2
@@ -130,24 +132,66 @@ def run_model(name, shapes, layers, reps, dev):
             "timing": "hipGraph replay of the pass", "eager_seconds": te, "eager_frac": byt / te / PEAK}
 
 
+def eager_per_launch(launch, steps, reps):
+    """bench.py's timing: a device spin covering the host's submission, 8 untimed lead
+    launches, then `steps` launches between HIP events on the launch stream; median
+    over `reps` of the per-launch time (s)."""
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    torch.cuda._sleep(2_000_000)
+    e1.record(st)
+    torch.cuda.synchronize()
+    cyc_per_us = 2_000_000 / max(e0.elapsed_time(e1) * 1e3, 1.0)
+    ts = []
+    for _ in range(reps):
+        torch.cuda._sleep(int(cyc_per_us * (40.0 * (steps + 8) + 200.0)))
+        for j in range(8):
+            launch(j - 8)
+        e0.record(st)
+        for i in range(steps):
+            launch(i)
+        e1.record(st)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e-3 / steps)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
 def run_single(name, m, n, dt, code, reps, dev, sets=16, steps=64):
+    """Single launches over `sets` rotating buffer sets.  Timed as bench.py times its
+    steps (eager launches behind a spin, ``us_per_launch``); the hipGraph replay of
+    the same launches is reported beside it (``graph_us_per_launch``): on ROCm 7.2 a
+    replay adds 1-3 us per 8192^2 kernel, as a system-scope release between eager
+    launches does (tools/c5_probe.py, profiles/r03/c5/)."""
     gen = torch.Generator(device=dev)
     gen.manual_seed(1)
     ws = [make_weight(m, n, dev, gen, dt) for _ in range(sets)]
     L = _lib.lib()
+
+    def launch(i):
+        q, a1, a2, o = ws[i % sets]
+        assert L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                                 o.data_ptr(), code, m, n, torch.cuda.current_stream().cuda_stream) == 0
+
+    for i in range(sets):  # every set touched once (TLB-warm, as resident weights are)
+        launch(i)
+    torch.cuda.synchronize()
+    t = eager_per_launch(launch, steps, reps)
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
-        sp = torch.cuda.current_stream().cuda_stream
         for i in range(steps):
-            q, a1, a2, o = ws[i % sets]
-            assert L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
-                                     o.data_ptr(), code, m, n, sp) == 0
-    t = timed(graph.replay, reps) / steps
+            launch(i)
+    tg = timed(graph.replay, reps) / steps
     ob = torch.empty((), dtype=dt).element_size()
     byt = alg_bytes(m, n, ob)
     checked = verify(ws[:min(sets, steps)], code)
-    return {"config": name, "verified": True, "verified_matrices": checked, "m": m, "n": n, "out_dtype": str(dt).replace("torch.", ""), "us_per_launch": t * 1e6,
-            "elements_per_s": m * n / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK}
+    fp = sets * (m * n // 2 + m * n * ob + m * n // 64)
+    return {"config": name, "verified": True, "verified_matrices": checked, "m": m, "n": n,
+            "out_dtype": str(dt).replace("torch.", ""), "sets": sets, "footprint_bytes": fp,
+            "us_per_launch": t * 1e6, "elements_per_s": m * n / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9,
+            "frac": byt / t / PEAK, "timing": "eager launches behind a spin (bench.py's method)",
+            "graph_us_per_launch": tg * 1e6, "graph_frac": byt / tg / PEAK}
 
 
 def run_bnb(name, m, n, reps, dev, sets=16, steps=64):
@@ -191,10 +235,13 @@ def main():
         torch.cuda.empty_cache()
     if "c4" in todo:
         for dt, code in ((torch.float16, _lib.F16), (torch.bfloat16, _lib.BF16), (torch.float32, _lib.F32)):
-            print(json.dumps(run_single("c4 4096x4096 dtype sweep", 4096, 4096, dt, code, args.reps, dev)), flush=True)
+            print(json.dumps(run_single("c4 4096x4096 dtype sweep", 4096, 4096, dt, code, args.reps, dev,
+                                        sets=13 if dt != torch.float32 else 8)), flush=True)
     if "c5" in todo:
+        # 4 sets = 675 MB: the flat HBM regime of bench.py's MIN_FOOTPRINT (past the
+        # Infinity Cache, short of the ~1.2 GB footprint where every launch pays ~10 %)
         print(json.dumps(run_single("c5 8192x8192 per-GPU unit", 8192, 8192, torch.bfloat16, _lib.BF16, args.reps, dev,
-                                    sets=8, steps=32)), flush=True)
+                                    sets=4, steps=64)), flush=True)
 
 
     if "big" in todo:

@@ -55,6 +55,27 @@ for stage in "$@"; do
             timeout -k 10 200 $PY bench.py --m 8192 --n 8192 --steps 64 --no-cpu-baseline $a > "$O/knob_$lab.json" 2>> "$O/knobs.err"
             python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['roofline']['launch_us_mean'],3), round(d['roofline']['frac'],4))" "$O/knob_$lab.json" "$lab"
         done ;;
+    gstamps)  # fused-GEMM phase stamps (tools/_build/libnf4dq_gstamps.so, built here)
+        for spec in ${GSTAMPS:-"14336,4096:32" "14336,4096:16" "14336,4096:1" "4096,4096:32" "4096,14336:32"}; do
+            timeout -k 10 200 $PY tools/gemm_stamps.py --shape ${spec%%:*} --m ${spec##*:} >> "$O/gemm_stamps.jsonl" 2>> "$O/gemm_stamps.err"
+        done
+        cat "$O/gemm_stamps.jsonl" ;;
+    dqab)  # interleaved dequant launch-config A/B: DQAB_ARGS passed to tools/dq_ab.py
+        timeout -k 10 400 $PY tools/dq_ab.py ${DQAB_ARGS:-} > "$O/dq_ab.jsonl" 2> "$O/dq_ab.err"; cat "$O/dq_ab.jsonl" ;;
+    gemmab)  # decode GEMM per launch, product vs the A/B libraries named in ABLIBS (tools/_build/libnf4dq_<x>.so)
+        timeout -k 10 300 $PY tools/gemm_ab.py ${GEMMAB_ARGS:-} >> "$O/gemm_ab.jsonl" 2>> "$O/gemm_ab.err"
+        for x in ${ABLIBS:-}; do
+            NF4DQ_LIB_PATH=tools/_build/libnf4dq_$x.so timeout -k 10 300 $PY tools/gemm_ab.py ${GEMMAB_ARGS:-} >> "$O/gemm_ab.jsonl" 2>> "$O/gemm_ab.err"
+        done
+        cat "$O/gemm_ab.jsonl" ;;
+    gemmtest)
+        timeout -k 10 600 $PY -m pytest tests/test_gpu_gemm.py tests/test_gpu_redzones.py tests/test_gpu_concurrency.py -x -q \
+            --timeout 300 --timeout-method thread > "$O/gemmtest.log" 2>&1 || { tail -30 "$O/gemmtest.log"; exit 1; }
+        tail -2 "$O/gemmtest.log" ;;
+    dqtest)
+        timeout -k 10 600 $PY -m pytest tests/test_gpu_parity.py tests/test_gpu_large.py tests/test_gpu_configs.py -x -q \
+            --timeout 300 --timeout-method thread > "$O/dqtest.log" 2>&1 || { tail -30 "$O/dqtest.log"; exit 1; }
+        tail -2 "$O/dqtest.log" ;;
     c5trace)
         trace configs_c5 nf4_flat_kernel 32 600 -- tools/bench_configs.py --configs c5
         trace bench_8192 nf4_flat_kernel 64 300 -- bench.py --m 8192 --n 8192 --steps 64 --no-cpu-baseline ;;

@@ -31,10 +31,10 @@ def main():
     ap.add_argument("--sets", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=64)
-    ap.add_argument("--tiles", default="4,8")
+    ap.add_argument("--tiles", default="4")
     ap.add_argument("--bpcu", default="0,1,2,4,8")
     ap.add_argument("--nt", default="1")
-    ap.add_argument("--flags", default="0", help="NF4DQ_CFG_* bits: 1 nt loads, 0x10..0x40 waves/WG, 0x100.. segments")
+    ap.add_argument("--flags", default="0", help="NF4DQ_CFG_A1_PREFETCH field: (log2 tiles) << 8, 0 = off")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     m, n, P = args.m, args.n, args.sets
