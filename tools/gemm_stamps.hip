@@ -7,7 +7,8 @@
 // 1 prologue barrier passed, 2 first strip / chunk consumed, 3 strip loop done,
 // 4 final barrier passed, 5 results stored (slab: drained), 6 tickets drawn (the
 // reducing wave only), 7 summed time in the partial-tile stores + barrier,
-// 8 summed time in the reducer's sums, 9 exit, 14 HW_ID, 15 XCC_ID.
+// 8 summed time in the reducer's sums, 9 exit, 10-12 prologue steps (register-resident
+// kernel: 11 x issued, 10 ring issued, 12 tables written), 14 HW_ID, 15 XCC_ID.
 // Built into tools/_build/libnf4dq_gstamps.so with the product's dequant and
 // host objects (tools/Makefile `gstamps`); read by tools/gemm_stamps.py.
 #include <hip/hip_runtime.h>

@@ -65,8 +65,9 @@ def main():
         wsz = (L.nf4_gemm_workspace_bytes_cfg(M, n, k, ctypes.byref(cfg)) if cfg else
                L.nf4_gemm_workspace_bytes(M, n, k))
         work = torch.zeros(max(wsz, 1 << 16), dtype=torch.uint8, device=dev)
-        rows = {key: [] for key in ("start", "pro", "first", "loop", "red_store_barrier", "red_sum", "final_barrier",
-                                    "store", "handoff", "end")}
+        rows = {key: [] for key in ("start", "pro", "pro_x_issue", "pro_ring_issue", "pro_tables", "pro_barrier",
+                                    "first", "loop", "red_store_barrier", "red_sum", "final_barrier", "store", "handoff",
+                                    "end")}
         spans = []
         for it in range(args.launches + 2):
             q, a1, a2 = ws[it % copies]
@@ -93,9 +94,14 @@ def main():
                 v = t[:, i].copy()
                 v[st[:, i] == 0] = np.nan
                 return v
-            s0, s1, s2, s3, s4, s5, s9 = (col(i) for i in (0, 1, 2, 3, 4, 5, 9))
+            s0, s1, s2, s3, s4, s5, s9, s10, s11, s12 = (col(i) for i in (0, 1, 2, 3, 4, 5, 9, 10, 11, 12))
+            s9 = np.where(np.isnan(s9), s5, s9)  # one-slice launches return after their y stores
             rows["start"].append(s0 - t0)
             rows["pro"].append(s1 - s0)
+            rows["pro_x_issue"].append(s11 - s0)
+            rows["pro_ring_issue"].append(s10 - s11)
+            rows["pro_tables"].append(s12 - s10)
+            rows["pro_barrier"].append(s1 - s12)
             rows["first"].append(s2 - s1)
             rows["loop"].append(s3 - s1)
             rows["red_store_barrier"].append(st[:, 7] / 100.0)
