@@ -721,6 +721,12 @@ __device__ __forceinline__ void xr_pair_mma(const u32x4& w0, const u32x4& w1, fl
     if constexpr (MT == 1) acc[0] += accb[0];
 }
 
+// Piece swizzle of the staged x rows (16-byte pieces 0..31 of a row's 512 bytes):
+// piece c of local row r sits at slot c ^ xr_xsw(r).  In each ds_read_b128 lane
+// group ({0-3,12-15,20-27}, ...: rows 0-3 and 12-15 of one 128-byte segment, rows
+// 4-11 of the next) the 16 lanes then hit 16 distinct 4-bank sets.
+__device__ __forceinline__ uint32_t xr_xsw(uint32_t r) { return r ^ ((((r + 4u) >> 3) & 1u) << 3); }
+
 template <int DT, int MT, int WV, int KPW, int D>
 __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) {
     extern __shared__ __attribute__((aligned(16))) f32x4 xr_smem[];  // all LDS dynamic (host: xr_lds_bytes)
@@ -753,20 +759,50 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     //    slower: 21.9 vs 20.3 us at M = 32 on 14336x4096, profiles/r03/gemm.)
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
     u32x4 xf[KPW][MT][4];
+    // Staged form (one 256-deep chunk, two row tiles, 8 waves): a lane's fragments are
+    // 128 contiguous bytes of one row, so a direct 16-byte load instruction touches 64
+    // lines (16 rows x 4 lanes) and the wave's 16 of them queue behind each other in
+    // the address path (the x issue was ~4.4 us of the prologue at M = 32,
+    // profiles/r03/gemm).  Instead each LDS-DMA instruction reads two rows' 512 bytes
+    // = 8 whole lines into the wave's own 8 KiB of LDS (row tile 0 in the reduction
+    // buffer, row tile 1 in the pair table's region, both free until the tables are
+    // written), and the fragments are read back with ds_read_b128.  Pieces are
+    // swizzled within a row (piece c at slot c ^ xr_xsw(row)) so the reads are
+    // conflict-free in every 16-lane group.
+    constexpr bool kStage = KPW == 2 && MT == 2 && R == 2;
+    const bool xlive = cw + (KPW == 1 ? 0u : 1u) < A.chunks;  // uniform: the wave's chunk inside K
+    if constexpr (kStage) {
+        if (xlive) {
+            const uint32_t rl = lane >> 5, slot = lane & 31u;
 #pragma unroll
-    for (int q = 0; q < KPW; ++q)
+            for (int mt = 0; mt < 2; ++mt) {
+                char* reg = reinterpret_cast<char*>(mt == 0 ? (void*)red : (void*)xr_smem) + wave * 8192u;
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            // k of fragment (q, s): 128 cw + 32 kh + 8 s (KPW 1), 128 cw + 256 (q / 2) + 64 kh
-            // + 32 (q % 2) + 8 s (256-deep sub-chunks) -- the weight dword's k (same permutation)
-            const uint32_t r = 16u * mt + nl;
-            const uint32_t c = cw + (KPW == 1 ? 0u : 2u * (uint32_t)(q / 2));
-            const uint32_t xoff = r < A.M && c + (KPW == 1 ? 0u : 1u) < A.chunks
-                                      ? (r * A.K + c * kChunkK + (KPW == 1 ? 32u : 64u) * kh + 32u * (q % 2)) * 2u
-                                      : kOob;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) xf[q][mt][s] = __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + 16u * s, 0, 0);
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t r = 16u * mt + 2u * i + rl;  // row of this lane's piece
+                    const uint32_t voff =
+                        r < A.M ? (r * A.K + cw * kChunkK) * 2u + 16u * (slot ^ xr_xsw(2u * i + rl)) : kOob;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rx, (__attribute__((address_space(3))) void*)(reg + 1024 * i), 16, voff, 0, 0, 0);
+                }
+            }
         }
+    } else {
+#pragma unroll
+        for (int q = 0; q < KPW; ++q)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                // k of fragment (q, s): 128 cw + 32 kh + 8 s (KPW 1), 128 cw + 256 (q / 2) + 64 kh
+                // + 32 (q % 2) + 8 s (256-deep sub-chunks) -- the weight dword's k (same permutation)
+                const uint32_t r = 16u * mt + nl;
+                const uint32_t c = cw + (KPW == 1 ? 0u : 2u * (uint32_t)(q / 2));
+                const uint32_t xoff = r < A.M && c + (KPW == 1 ? 0u : 1u) < A.chunks
+                                          ? (r * A.K + c * kChunkK + (KPW == 1 ? 32u : 64u) * kh + 32u * (q % 2)) * 2u
+                                          : kOob;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) xf[q][mt][s] = __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + 16u * s, 0, 0);
+            }
+    }
     __builtin_amdgcn_sched_barrier(0);  // issue order = wait order: x, then the ring slot by slot
     NF4_GSTAMP(11);
     XSlot<KPW> ring[D];
@@ -778,6 +814,23 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
         __builtin_amdgcn_sched_barrier(0);
     }
     NF4_GSTAMP(10);
+    if constexpr (kStage) {
+        // the x DMA went out before the ring's D x 4 loads: wait for it alone (the
+        // compiler does not order LDS-DMA writes before these LDS reads by itself)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * D) : "memory");
+        // fragment (q, s) of row tile mt = piece 8 kh + 4 q + s of row 16 mt + nl
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            const char* reg = reinterpret_cast<const char*>(mt == 0 ? (void*)red : (void*)xr_smem) + wave * 8192u;
+            const bool rok = xlive && 16u * mt + nl < A.M;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(reg + nl * 512u + 16u * ((8u * kh + p) ^ xr_xsw(nl)));
+                xf[p >> 2][mt][p & 3] = rok ? v : u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+        __syncthreads();  // every wave's fragments out of the pair table's region before the tables
+    }
     write_lut(lut);
     if constexpr (KPW >= 2) {  // tables while the loads fly (as the streaming kernels)
         if (tid < 256u) qtab[tid] = (float)tid / 127.0f;  // IEEE division (:45)

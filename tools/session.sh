@@ -80,9 +80,29 @@ for stage in "$@"; do
         trace configs_c5 nf4_flat_kernel 32 600 -- tools/bench_configs.py --configs c5
         trace bench_8192 nf4_flat_kernel 64 300 -- bench.py --m 8192 --n 8192 --steps 64 --no-cpu-baseline ;;
     rocprof)
-        trace bench nf4_flat_kernel 200 300 -- bench.py --steps 200 --no-cpu-baseline
+        trace bench nf4_flat_kernel 200 300 -- bench.py --steps 200 --no-cpu-baseline --no-c5
         python3 tools/rocprof_summary.py "$O/prof_bench" nf4_flat_kernel "$O/rocprof_bench_summary.json" \
             "$O/rocprof_bench_kernel_stats.csv" --last 200 > /dev/null ;;
+    pmc)  # headline HBM traffic (FETCH_SIZE / WRITE_SIZE passes, calibrated) + decode-GEMM SQ counters
+        test -f tools/_build/libpmccalib.so
+        timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc" -o fetch -- \
+            python3 -u tools/pmc_probe.py > "$O/pmc_fetch.log" 2>&1
+        timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc" -o write -- \
+            python3 -u tools/pmc_probe.py > "$O/pmc_write.log" 2>&1
+        python3 tools/pmc_traffic.py "$O/pmc" "$O/pmc_traffic.json" > "$O/pmc_traffic.log" 2>&1
+        cat "$O/pmc_traffic.json"
+        GA="tools/gemm_ab.py --ms ${PMC_M:-32} --shapes ${PMC_SHAPE:-14336,4096} --budget-mb 512"
+        timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM --output-format csv -d "$O/pmcg_a" -o a -- \
+            python3 -u $GA > "$O/pmcg_a.log" 2>&1
+        timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INST_LEVEL_VMEM \
+            SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_VMEM_TA_ADDR_FIFO_FULL \
+            --output-format csv -d "$O/pmcg_b" -o b -- python3 -u $GA > "$O/pmcg_b.log" 2>&1
+        python3 tools/pmc_gemm.py "$O" nf4_gemm_xr_kernel nf4_gemm_persist_kernel nf4_gemm_stream_kernel > "$O/pmc_gemm.jsonl"
+        cat "$O/pmc_gemm.jsonl" ;;
+    gemmpass)  # the Llama-3-8B decode pass, fused GEMM (tools/bench_gemm.py)
+        timeout -k 10 500 $PY tools/bench_gemm.py --ms ${GEMM_MS:-1,4,8,12,16,24,32} > "$O/bench_gemm.jsonl" 2> "$O/bench_gemm.err"
+        cat "$O/bench_gemm.jsonl" ;;
     configs)
         timeout -k 10 900 $PY tools/bench_configs.py > "$O/configs.jsonl" 2> "$O/configs.err"; cat "$O/configs.jsonl" ;;
     *)
