@@ -729,14 +729,17 @@ __device__ __forceinline__ uint32_t xr_xsw(uint32_t r) { return r ^ ((((r + 4u) 
 
 template <int DT, int MT, int WV, int KPW, int D>
 __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) {
-    extern __shared__ __attribute__((aligned(16))) f32x4 xr_smem[];  // all LDS dynamic (host: xr_lds_bytes)
-    // 256-deep chunks: the pair table (64 KiB) and the q/127 table lead the region
-    constexpr int kPt = KPW >= 2 ? (256 * 32 * 8 + 1024) / 16 : 0;  // in f32x4
-    f32x2* ptab = reinterpret_cast<f32x2*>(xr_smem);
-    float* qtab = reinterpret_cast<float*>(xr_smem + (256 * 32 * 8) / 16);
+    extern __shared__ __attribute__((aligned(16))) f32x4 xr_smem[];  // dynamic part (host: xr_lds_dynamic)
+    // 256-deep chunks: the pair table (64 KiB) and the q/127 table, static so that the
+    // lookups' addresses need no base added (one VALU per two weights less than in a
+    // dynamic region, whose base the compiler adds as a late-resolved 0)
+    __shared__ __attribute__((aligned(16))) f32x2 xr_ptab[KPW >= 2 ? 256 * 32 : 2];
+    __shared__ float xr_qtab[KPW >= 2 ? 256 : 4];
+    f32x2* ptab = xr_ptab;
+    float* qtab = xr_qtab;
     // partial tiles meet once per R strips (8 waves: two strips per barrier)
     constexpr int R = WV == 8 && D % 2 == 0 ? 2 : 1;
-    f32x4* red = xr_smem + kPt;                              // [2][R][WV][MT][64] partial tiles
+    f32x4* red = xr_smem;                                    // [2][R][WV][MT][64] partial tiles
     float* lut = reinterpret_cast<float*>(red + 2 * R * WV * MT * 64);  // 16 codes
     uint32_t* last_flags = reinterpret_cast<uint32_t*>(lut + 16);        // [64] split-K tickets drawn last
     float* held = reinterpret_cast<float*>(last_flags + 64);            // [T][16 MT][16] fp32 results
@@ -776,7 +779,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
             const uint32_t rl = lane >> 5, slot = lane & 31u;
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
-                char* reg = reinterpret_cast<char*>(mt == 0 ? (void*)red : (void*)xr_smem) + wave * 8192u;
+                char* reg = reinterpret_cast<char*>(mt == 0 ? (void*)red : (void*)xr_ptab) + wave * 8192u;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const uint32_t r = 16u * mt + 2u * i + rl;  // row of this lane's piece
@@ -821,7 +824,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
         // fragment (q, s) of row tile mt = piece 8 kh + 4 q + s of row 16 mt + nl
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
-            const char* reg = reinterpret_cast<const char*>(mt == 0 ? (void*)red : (void*)xr_smem) + wave * 8192u;
+            const char* reg = reinterpret_cast<const char*>(mt == 0 ? (void*)red : (void*)xr_ptab) + wave * 8192u;
             const bool rok = xlive && 16u * mt + nl < A.M;
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
@@ -2014,11 +2017,16 @@ static int launch_xs(const HostMat* mats, int count, const void* x, int64_t M, i
 // Register-resident kernel: grid = ksplit x (strip groups of T strips); T from
 // the CUs the launch can hold at once (one 16-wave workgroup per CU), at most 64
 // (ticket flags) and within LDS.
-static uint32_t xr_lds_bytes(int64_t M, int waves, int kpw, uint32_t T) {
+static uint32_t xr_lds_static(int kpw) {  // pair table + q/127 (256-deep chunks), static in the kernel
+    return kpw >= 2 ? 256u * 32u * 8u + 1024u : 64u;
+}
+static uint32_t xr_lds_dynamic(int64_t M, int waves, uint32_t T) {
     const uint32_t mt = M > 16 ? 2u : 1u;
     const uint32_t r = waves == 8 ? 2u : 1u;  // strips per reduction group (kernel's R; depth is even)
-    const uint32_t tables = kpw >= 2 ? 256u * 32u * 8u + 1024u : 0u;  // pair table + q/127 (256-deep chunks)
-    return tables + 2u * r * (uint32_t)waves * mt * 1024u + 64u + 256u + T * mt * 1024u;  // partials, codes, flags, held
+    return 2u * r * (uint32_t)waves * mt * 1024u + 64u + 256u + T * mt * 1024u;  // partials, codes, flags, held
+}
+static uint32_t xr_lds_bytes(int64_t M, int waves, int kpw, uint32_t T) {
+    return xr_lds_static(kpw) + xr_lds_dynamic(M, waves, T);
 }
 
 static uint32_t xr_per_wg(int64_t M, int64_t strips, const nf4_gemm_cfg& c) {
@@ -2065,13 +2073,14 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
     A.per_wg = xr_per_wg(M, strips, cfg);
     const uint32_t groups = (strips + A.per_wg - 1) / A.per_wg;
     const dim3 grid(groups * ks), block(64 * cfg.waves);
-    const uint32_t lds = xr_lds_bytes(M, cfg.waves, cfg.strips, A.per_wg);
+    const uint32_t lds = xr_lds_dynamic(M, cfg.waves, A.per_wg);
 #define NF4_R1(DT_, MT_, W_, KPW_, D_)                                                                               \
     do {                                                                                                             \
         static bool attr_ = false; /* dynamic LDS above 64 KiB needs the opt-in */                                   \
         if (!attr_) {                                                                                                \
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_xr_kernel<DT_, MT_, W_, KPW_, D_>),    \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu);                   \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,                                    \
+                                      (int)(kLdsPerCu - xr_lds_static(KPW_)));                                       \
             attr_ = true;                                                                                            \
         }                                                                                                            \
         hipLaunchKernelGGL((nf4_gemm_xr_kernel<DT_, MT_, W_, KPW_, D_>), grid, block, lds, st, A);                   \
