@@ -1,0 +1,32 @@
+// Ablation builds of the register-resident decode-GEMM kernel (tools only; timing,
+// never correctness).  Redefines one of the NF4_XR_* hooks of nf4_gemm.hip (selected
+// by -DABL_<part>) and includes the product source; tools/Makefile `ablate` links
+// each variant with the product's dequant and host objects into
+// tools/_build/libnf4dq_abl_<part>.so, timed by tools/gemm_ab.py.
+//   ABL_NOLUT   codes made from the address bits instead of the pair-table read
+//   ABL_NOWLOAD weight "loads" made from their offsets (no memory traffic)
+//   ABL_NOMMA   no MFMAs (operands kept alive)
+//   ABL_NORED   no in-LDS reduction of the K-partial tiles (no per-strip barriers)
+//   ABL_NOHAND  no split-K hand-off (no slab stores, tickets or last-arriver sums)
+#include <hip/hip_runtime.h>
+
+#if defined(ABL_NOLUT)
+#define NF4_XR_LOOKUP(pt_, addr_, wd_) \
+    (f32x2{__uint_as_float(((addr_) & 0xFFFFu) | 0x3F000000u), __uint_as_float(((wd_) & 0xFFFFu) | 0x3E000000u)})
+#elif defined(ABL_NOWLOAD)
+#define NF4_XR_WLOAD(rsrc_, off_) (u32x4{(off_), (off_) * 3u, (off_) ^ 0x5A5A5A5Au, (off_) + 0x01010101u})
+#elif defined(ABL_NOMMA)
+#define NF4_XR_MMA_ON 0
+#define NF4_XR_RED_ON 1
+#define NF4_XR_HANDOFF_ON 1
+#elif defined(ABL_NORED)
+#define NF4_XR_MMA_ON 1
+#define NF4_XR_RED_ON 0
+#define NF4_XR_HANDOFF_ON 1
+#elif defined(ABL_NOHAND)
+#define NF4_XR_MMA_ON 1
+#define NF4_XR_RED_ON 1
+#define NF4_XR_HANDOFF_ON 0
+#endif
+
+#include "../nf4_triton_dequantization_amd/csrc/nf4_gemm.hip"
