@@ -52,12 +52,33 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 #define NF4_GSTAMP_INIT(waves_) ((void)0)
 #endif
 
+// Ablation hooks of the pair-table kernels (register-resident, streaming,
+// persistent): the product operation by default.  tools/gemm_ablate.hip redefines
+// them to time a kernel with one part removed (its results are then wrong: timing
+// only, never in the library).
+//   NF4_ABL_LOOKUP(pt, addr, wd)  pair-table read of the two codes of a byte
+//   NF4_ABL_WLOAD(rsrc, off)      16-byte weight load of the ring
+//   NF4_ABL_MMA_ON                the MFMAs (operands kept alive when off)
+//   NF4_ABL_RED_ON / _HANDOFF_ON  register-resident kernel: in-LDS K reduction / split-K hand-off
+#ifndef NF4_ABL_LOOKUP
+#define NF4_ABL_LOOKUP(pt_, addr_, wd_) (*reinterpret_cast<const f32x2*>((pt_) + (addr_)))
+#endif
+#ifndef NF4_ABL_WLOAD
+#define NF4_ABL_WLOAD(rsrc_, off_) __builtin_amdgcn_raw_buffer_load_b128((rsrc_), (off_), 0, 0)
+#endif
+#ifndef NF4_ABL_MMA_ON
+#define NF4_ABL_MMA_ON 1
+#define NF4_ABL_RED_ON 1
+#define NF4_ABL_HANDOFF_ON 1
+#endif
+
 // Split-K hand-off, in the HIP memory model with relaxed agent-scope atomics
 // only (no fence, no cache-policy assumption).  A slab entry is one 64-bit word
 // holding the fp32 partials of two adjacent columns (c, c + 1; c even), each as
 // the bitwise NOT of its bits: 0 = empty (the zero-filled workspace's state),
-// both halves nonzero = written.  Each K slice stores its partials with atomic
-// stores, then one lane draws a ticket on the strip's counter (atomic add); the
+// both halves nonzero = written.  Each K slice issues its partials as atomic
+// stores, then one lane draws a ticket on the strip's counter (atomic add; no wait
+// for the stores to complete -- the ticket only elects the reducer); the
 // slice drawing ksplit - 1 resets the counter and reduces: it reads every slice's
 // entries with atomic loads, waiting per entry until it is written (per-location
 // coherence: it sees the store once it is made; the entry held 0 since the
@@ -656,7 +677,7 @@ __device__ __forceinline__ void xslot_issue(const GemmArgs& A, uint32_t strip, b
         constexpr int WQ = KPW == 1 ? 1 : 2;  // 16-byte weight loads per sub-chunk
 #pragma unroll
         for (int q = 0; q < WQ; ++q)
-            s.w[WQ * h + q] = __builtin_amdgcn_raw_buffer_load_b128(rw, (w0 + 16u * q) | oob, 0, 0);
+            s.w[WQ * h + q] = NF4_ABL_WLOAD(rw, (w0 + 16u * q) | oob);
         s.qa[h] = __builtin_amdgcn_raw_buffer_load_b8(ra1, fmodu(r0 * A.bpr + 2u * c + ln.b1, Mt.nb) | oob, 0, 0);  // (:173-177)
         s.qb[h] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
             ra2, (fmodu(r0 * A.groups + (c >> 1) + ln.b2, Mt.n2) * 4u) | oob, 0, 0));  // (:40-41, :183-186)
@@ -685,7 +706,7 @@ __device__ __forceinline__ void xr_pair_mma(const u32x4& w0, const u32x4& w1, fl
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const uint32_t addr = __builtin_amdgcn_perm(wd, slot8, 0x0C0C0000u | ((4u + b) << 8));
-            v[st][b] = *reinterpret_cast<const f32x2*>(pt + addr);
+            v[st][b] = NF4_ABL_LOOKUP(pt, addr, wd);
         }
     };
 #pragma unroll
@@ -709,7 +730,9 @@ __device__ __forceinline__ void xr_pair_mma(const u32x4& w0, const u32x4& w1, fl
         for (int mt = 0; mt < MT; ++mt) {
             f32x4& c = (MT == 1 && (st & 1)) ? accb[0] : acc[mt];
             const u32x4 a = xf[st >> 2][mt][st & 3];
-            if constexpr (DT == NF4DQ_BF16) {
+            if constexpr (!NF4_ABL_MMA_ON) {
+                asm volatile("" ::"v"(a), "v"(bq));
+            } else if constexpr (DT == NF4DQ_BF16) {
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, bq),
                                                             c, 0, 0, 0);
             } else {
@@ -894,7 +917,12 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
             __builtin_amdgcn_sched_barrier(0);
             if (d % R != R - 1) continue;  // the group's partials meet after its last strip
             const uint32_t tg = t + 1u - (uint32_t)R;  // first strip of the group
-            if (tg < nst) {  // uniform
+            if constexpr (!NF4_ABL_RED_ON) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) asm volatile("" ::"v"(accs[r][mt]));
+            } else if (tg < nst) {  // uniform
                 NF4_GSPAN_BEGIN();
                 // red slot of strip u: ((u / R) & 1) * R + u % R (two groups in flight)
 #pragma unroll
@@ -950,13 +978,16 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
         NF4_GSTAMP(5);
         return;
     }
+    if constexpr (!NF4_ABL_HANDOFF_ON) return;
     // slab [ks][M][ncols] entries (strip s at columns 16 s): splitk_ticket / splitk_reduce
     for (uint32_t e = tid; e < nst * rows * 8u; e += 64u * WV) {  // column pairs
         const uint32_t t = e / (rows * 8u), rem = e - t * rows * 8u, m = rem >> 3, c = 2u * (rem & 7u);
         const float* h = held + t * (16u * MT * 16u) + m * 16u + c;
         slab_put2(A.slab, slab_entry(ks, A.M, m, A.ncols, (s0 + t) * 16u + c), h[0], h[1]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's entries are out before its tickets
+    // no wait for the entries' write acknowledgements before the tickets: the
+    // reducer polls every entry until it is written, so a ticket only says who sums
+    // (waiting cost a memory round trip per launch)
     NF4_GSTAMP(5);
     __syncthreads();
     if (tid < nst) last_flags[tid] = splitk_ticket(&A.counters[s0 + tid], S);  // one ticket per strip; nst <= 64
@@ -1041,8 +1072,8 @@ __device__ __forceinline__ void sslot_issue(const StreamArgs& A, const StreamMat
     // the waitcnt pass sees one straight-line ring
     const uint32_t oob = valid ? 0u : kOob;
     const uint32_t woff = (row * (A.K >> 1) + c * 128u + kh * 32u) | oob;
-    s.w0 = __builtin_amdgcn_raw_buffer_load_b128(rw, woff, 0, 0);
-    s.w1 = __builtin_amdgcn_raw_buffer_load_b128(rw, woff + 16u, 0, 0);
+    s.w0 = NF4_ABL_WLOAD(rw, woff);
+    s.w1 = NF4_ABL_WLOAD(rw, woff + 16u);
     if constexpr (!VS) {
         // block 4c + kh of the row; its nested group is c (reference wraps, :173-186)
         const uint32_t i1 = fmodu(row * A.bpr + 4u * c + kh, Mt.nb) | oob;
@@ -1077,7 +1108,7 @@ __device__ __forceinline__ void sslot_mma(const SSlot& s, uint32_t qa, float qb,
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const uint32_t addr = __builtin_amdgcn_perm(wd, slot8, 0x0C0C0000u | ((4u + b) << 8));
-            v[st][b] = *reinterpret_cast<const f32x2*>(pt + addr);
+            v[st][b] = NF4_ABL_LOOKUP(pt, addr, wd);
         }
     };
 #pragma unroll
@@ -1099,7 +1130,9 @@ __device__ __forceinline__ void sslot_mma(const SSlot& s, uint32_t qa, float qb,
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
             f32x4& c = (st & 1) ? accb[mt] : acc[mt];
-            if constexpr (DT == NF4DQ_BF16) {
+            if constexpr (!NF4_ABL_MMA_ON) {
+                asm volatile("" ::"v"(a[mt]), "v"(bq));
+            } else if constexpr (DT == NF4DQ_BF16) {
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[mt]),
                                                             __builtin_bit_cast(bf16x8, bq), c, 0, 0, 0);
             } else {
@@ -1369,8 +1402,8 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     auto issue_w = [&](SSlot& sl, int s, bool valid) {
         const uint32_t c = cbase + l0 + rr2 * P + (uint32_t)s;
         const uint32_t woff = (gi.row * (A.K >> 1) + c * 128u + kh * 32u) | (valid ? 0u : kOob);
-        sl.w0 = __builtin_amdgcn_raw_buffer_load_b128(gi.rw, woff, 0, 0);
-        sl.w1 = __builtin_amdgcn_raw_buffer_load_b128(gi.rw, woff + 16u, 0, 0);
+        sl.w0 = NF4_ABL_WLOAD(gi.rw, woff);
+        sl.w1 = NF4_ABL_WLOAD(gi.rw, woff + 16u);
     };
     auto advance = [&]() {  // uniform
         if (++rr2 == rounds) {
@@ -1509,7 +1542,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         const uint32_t gstrip = Mt.strip_begin + (sgi - Mt.sg_begin) * A.T + t;
         slab_put2(A.slab, slab_entry(ks, A.M, rem2 >> 4, A.ncols, gstrip * 16u + (rem2 & 15u)), o32[i], o32[i + 1]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's entries are out before its tickets
+    // (no wait for the entries' write acknowledgements: the reducer polls them)
     __syncthreads();
     for (uint32_t ito = wave; ito < mine; ito += W) {
         const uint32_t sgi = j0 + ito * G;

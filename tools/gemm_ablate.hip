@@ -1,5 +1,5 @@
-// Ablation builds of the register-resident decode-GEMM kernel (tools only; timing,
-// never correctness).  Redefines one of the NF4_XR_* hooks of nf4_gemm.hip (selected
+// Ablation builds of the pair-table decode-GEMM kernels (tools only; timing,
+// never correctness).  Redefines one of the NF4_ABL_* hooks of nf4_gemm.hip (selected
 // by -DABL_<part>) and includes the product source; tools/Makefile `ablate` links
 // each variant with the product's dequant and host objects into
 // tools/_build/libnf4dq_abl_<part>.so, timed by tools/gemm_ab.py.
@@ -11,22 +11,22 @@
 #include <hip/hip_runtime.h>
 
 #if defined(ABL_NOLUT)
-#define NF4_XR_LOOKUP(pt_, addr_, wd_) \
+#define NF4_ABL_LOOKUP(pt_, addr_, wd_) \
     (f32x2{__uint_as_float(((addr_) & 0xFFFFu) | 0x3F000000u), __uint_as_float(((wd_) & 0xFFFFu) | 0x3E000000u)})
 #elif defined(ABL_NOWLOAD)
-#define NF4_XR_WLOAD(rsrc_, off_) (u32x4{(off_), (off_) * 3u, (off_) ^ 0x5A5A5A5Au, (off_) + 0x01010101u})
+#define NF4_ABL_WLOAD(rsrc_, off_) (u32x4{(off_), (off_) * 3u, (off_) ^ 0x5A5A5A5Au, (off_) + 0x01010101u})
 #elif defined(ABL_NOMMA)
-#define NF4_XR_MMA_ON 0
-#define NF4_XR_RED_ON 1
-#define NF4_XR_HANDOFF_ON 1
+#define NF4_ABL_MMA_ON 0
+#define NF4_ABL_RED_ON 1
+#define NF4_ABL_HANDOFF_ON 1
 #elif defined(ABL_NORED)
-#define NF4_XR_MMA_ON 1
-#define NF4_XR_RED_ON 0
-#define NF4_XR_HANDOFF_ON 1
+#define NF4_ABL_MMA_ON 1
+#define NF4_ABL_RED_ON 0
+#define NF4_ABL_HANDOFF_ON 1
 #elif defined(ABL_NOHAND)
-#define NF4_XR_MMA_ON 1
-#define NF4_XR_RED_ON 1
-#define NF4_XR_HANDOFF_ON 0
+#define NF4_ABL_MMA_ON 1
+#define NF4_ABL_RED_ON 1
+#define NF4_ABL_HANDOFF_ON 0
 #endif
 
 #include "../nf4_triton_dequantization_amd/csrc/nf4_gemm.hip"
