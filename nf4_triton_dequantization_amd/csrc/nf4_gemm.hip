@@ -109,6 +109,36 @@ __device__ __forceinline__ void slab_put_lane(uint64_t* slab, uint32_t e, float 
     if (valid && !(col & 1u)) slab_put2(slab, e, v, nb);
 }
 
+// Poll the entries of v[][] that are not written yet, all of them per round (one
+// memory round trip per round, not one per entry), at most kSpinMax rounds; an
+// entry still empty then reads as the NOT of two NaNs (a wrong result, never a
+// hung GPU).  Entries not to read are ~0 (full) on entry.
+template <int KK, int KU>
+__device__ __forceinline__ void splitk_poll(uint64_t* slab, uint32_t sstride, uint32_t k0, const uint32_t (&idx)[KU],
+                                            uint64_t (&v)[KK][KU]) {
+    for (int tries = 0; tries < kSpinMax; ++tries) {
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int j = 0; j < KK; ++j)
+#pragma unroll
+            for (int u = 0; u < KU; ++u)
+                if (!slab_full(v[j][u]))
+                    v[j][u] = __hip_atomic_load(slab + (k0 + j) * sstride + idx[u], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < KK; ++j)
+#pragma unroll
+            for (int u = 0; u < KU; ++u) ok = ok && slab_full(v[j][u]);
+        if (__all(ok)) return;
+    }
+#pragma unroll
+    for (int j = 0; j < KK; ++j)
+#pragma unroll
+        for (int u = 0; u < KU; ++u)
+            if (!slab_full(v[j][u])) v[j][u] = 0x803FFFFF803FFFFFull;  // NOT of two NaNs
+}
+
 __device__ __forceinline__ bool splitk_ticket(uint32_t* ctr, uint32_t ksplit) {
     const uint32_t t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t != ksplit - 1u) return false;
@@ -151,19 +181,7 @@ __device__ __forceinline__ void splitk_reduce(uint64_t* slab, uint32_t ksplit, u
                                    : ~0ull;
                     ok = ok && slab_full(v[j][u]);
                 }
-            if (!__all(ok)) {  // rare: an entry not written yet -- poll it
-#pragma unroll
-                for (int j = 0; j < kK; ++j)
-#pragma unroll
-                    for (int u = 0; u < kU; ++u) {
-                        uint64_t* ep = slab + (k0 + j) * sstride + idx[u];
-                        for (int tries = 0; !slab_full(v[j][u]) && tries < kSpinMax; ++tries) {
-                            __builtin_amdgcn_s_sleep(1);
-                            v[j][u] = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                        if (!slab_full(v[j][u])) v[j][u] = 0x803FFFFF803FFFFFull;  // NOT of two NaNs
-                    }
-            }
+            if (!__all(ok)) splitk_poll<kK, kU>(slab, sstride, k0, idx, v);  // entries not written yet
 #pragma unroll
             for (int j = 0; j < kK; ++j) {
                 if (k0 + j >= ksplit) break;  // uniform
