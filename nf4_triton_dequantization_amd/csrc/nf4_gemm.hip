@@ -732,11 +732,16 @@ __device__ __forceinline__ void xr_pair_mma(const u32x4& w0, const u32x4& w1, fl
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
         if (st + LA < 8) issue(st + LA);
-        // required for correctness, not speed: without it the scheduler interleaves
-        // the next refill's scalar loads (lgkmcnt, completing out of order) with these
-        // counted LDS waits, and every strip after a workgroup's first came out wrong
-        // (tools/xr_probe.py)
-        __builtin_amdgcn_sched_barrier(0);
+        // (Round 2 had a scheduling barrier here after wrong strips were seen beyond a
+        // workgroup's first.  Its stated cause -- scalar loads completing out of order
+        // under counted LDS waits -- is not in the ISA: a scan of every s_waitcnt of
+        // this kernel, at the commit that added the barrier and now, with and without
+        // it, finds no counted lgkmcnt wait while a scalar load is outstanding.  Without
+        // it the current kernel passes tools/xr_probe.py (58 configurations, 41 with
+        // several strips per workgroup) and the GEMM suite, and is 0.1-0.4 us faster
+        // per launch (profiles/r03/gemm/xr_no_sched_barrier.jsonl);
+        // test_xr_multi_strip_workgroups keeps several strips per workgroup under test
+        // at any CU count.)
         uint32_t bw[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {

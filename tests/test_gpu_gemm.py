@@ -213,6 +213,37 @@ def test_every_decomposition_agrees_with_oracle(coracle, gpu, dt, M, N, K):
     assert ran >= 12
 
 
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,K,kpw", [(32, 4096, 2), (17, 4096, 2), (32, 2048, 1), (24, 4096, 4)])
+def test_xr_multi_strip_workgroups(coracle, gpu, dt, M, K, kpw):
+    """The register-resident kernel with several 16-column strips per workgroup, at
+    any CU count: N is sized from the device's CUs so that every workgroup walks >= 3
+    strips (its ring refills, partial-tile reduction groups and cached weight
+    descriptors all cross strip boundaries)."""
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    waves = 8
+    ks = -(-(K // 128) // (waves * kpw))
+    # the library's grid (xr_per_wg): one workgroup per CU, two for 128-deep chunks
+    wg_per_slice = max(1, cus * (2 if kpw == 1 else 1) // ks)
+    N = 16 * 3 * wg_per_slice         # >= 3 strips per workgroup
+    N = -(-N // 64) * 64
+    assert (N // 16) / wg_per_slice >= 3
+    packed, a1, a2 = O.make_inputs(N, K, seed=N + K + M + kpw, a2_kind="normal")
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16)
+    t = (torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu))
+    xt, xb = _x_bits(M, K, dt, seed=M * 3 + kpw)
+    x = xt.to(gpu)
+    y = torch.full((M, N), float("nan"), dtype=x.dtype, device=gpu)
+    cfg = _lib.GemmCfg(_lib.GEMM_XR, waves, 2, ks, kpw)
+    rc = _gemm_cfg_call(L, _lib, x, t, y, _lib.BF16 if dt == "bf16" else _lib.F16, N, K, cfg)
+    assert rc == 0, rc
+    assert not bool(torch.isnan(y).any())
+    _check(y, xb, W, dt)
+
+
 def test_invalid_decompositions_rejected(gpu):
     from nf4_triton_dequantization_amd import _lib
 
