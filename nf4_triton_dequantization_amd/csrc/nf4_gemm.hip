@@ -9,15 +9,22 @@
 // once (0.5 B/element) and dequantized in registers -- the roofline is HBM on
 // the packed weight, not on a 2 B/element bf16 copy.
 //
-// Two kernels (host choice in default_gemm_cfg, explicit in nf4_gemm_ref_cfg):
+// Five kernels (host choice in default_gemm_cfg, explicit in nf4_gemm_ref_cfg):
 //  * nf4_gemm_smallm_kernel -- K % 128 == 0; 128-deep chunks, a lane loads 16
 //    packed bytes of its weight row (one 64-block, one scale) and the matching
 //    activation fragments from global memory; waves of a workgroup split K and
-//    meet in LDS.
+//    meet in LDS.  The fallback for any shape the others do not take.
+//  * nf4_gemm_xs_kernel -- shared-activation form of the 128-deep kernel: the
+//    x slice staged once per workgroup in LDS, one strip per wave.
+//  * nf4_gemm_xr_kernel -- register-resident x (16 < M <= 32, K % 256 == 0):
+//    each wave holds its K chunk's x fragments for the whole launch and walks
+//    the workgroup's column strips with a register ring of weight chunks.
 //  * nf4_gemm_stream_kernel -- K % 256 == 0 (every Llama shape); 256-deep
 //    chunks (one 128-byte line per weight row), activations staged in LDS,
 //    a register ring of weight chunks, pair-table dequant (see its comments).
-// Both use the same k permutation on A and B fragments (a lane's packed dword
+//  * nf4_gemm_persist_kernel -- the streaming body with one workgroup per CU
+//    walking strip groups (M <= 16), the ring running on across groups.
+// All use the same k permutation on A and B fragments (a lane's packed dword
 // is exactly its MFMA B fragment of one step), so no shuffle is needed.  K
 // slices over workgroups (ksplit > 1) write fp32 partials to a workspace slab;
 // the last workgroup to finish a column strip (ticket counter) sums the slices
@@ -60,6 +67,16 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 //   NF4_ABL_WLOAD(rsrc, off)      16-byte weight load of the ring
 //   NF4_ABL_MMA_ON                the MFMAs (operands kept alive when off)
 //   NF4_ABL_RED_ON / _HANDOFF_ON  register-resident kernel: in-LDS K reduction / split-K hand-off
+//   NF4_ABL_X_ON                  register-resident kernel: the x fragments' global loads
+//   NF4_ABL_SLOAD(rsrc, off, b8)  register-resident kernel: absmax byte / nested scale gather
+#ifndef NF4_ABL_X_ON
+#define NF4_ABL_X_ON 1
+#endif
+#ifndef NF4_ABL_SLOAD
+#define NF4_ABL_SLOAD(rsrc_, off_, b8_)                                                       \
+    ((b8_) ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8((rsrc_), (off_), 0, 0) \
+           : __builtin_amdgcn_raw_buffer_load_b32((rsrc_), (off_), 0, 0))
+#endif
 #ifndef NF4_ABL_LOOKUP
 #define NF4_ABL_LOOKUP(pt_, addr_, wd_) (*reinterpret_cast<const f32x2*>((pt_) + (addr_)))
 #endif
@@ -696,9 +713,9 @@ __device__ __forceinline__ void xslot_issue(const GemmArgs& A, uint32_t strip, b
 #pragma unroll
         for (int q = 0; q < WQ; ++q)
             s.w[WQ * h + q] = NF4_ABL_WLOAD(rw, (w0 + 16u * q) | oob);
-        s.qa[h] = __builtin_amdgcn_raw_buffer_load_b8(ra1, fmodu(r0 * A.bpr + 2u * c + ln.b1, Mt.nb) | oob, 0, 0);  // (:173-177)
-        s.qb[h] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-            ra2, (fmodu(r0 * A.groups + (c >> 1) + ln.b2, Mt.n2) * 4u) | oob, 0, 0));  // (:40-41, :183-186)
+        s.qa[h] = (uint8_t)NF4_ABL_SLOAD(ra1, fmodu(r0 * A.bpr + 2u * c + ln.b1, Mt.nb) | oob, true);  // (:173-177)
+        s.qb[h] = __uint_as_float(
+            NF4_ABL_SLOAD(ra2, (fmodu(r0 * A.groups + (c >> 1) + ln.b2, Mt.n2) * 4u) | oob, false));  // (:40-41, :183-186)
     }
 }
 
@@ -821,7 +838,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     constexpr bool kStage = KPW == 2 && MT == 2 && R == 2;
     const bool xlive = cw + (KPW == 1 ? 0u : 1u) < A.chunks;  // uniform: the wave's chunk inside K
     if constexpr (kStage) {
-        if (xlive) {
+        if (xlive && NF4_ABL_X_ON) {
             const uint32_t rl = lane >> 5, slot = lane & 31u;
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {

@@ -8,14 +8,32 @@
 //   ABL_NOMMA   no MFMAs (operands kept alive)
 //   ABL_NORED   no in-LDS reduction of the K-partial tiles (no per-strip barriers)
 //   ABL_NOHAND  no split-K hand-off (no slab stores, tickets or last-arriver sums)
+//   ABL_NOX     register-resident kernel: no global loads of the x fragments
+//   ABL_NOSCALE register-resident kernel: no absmax byte / nested scale gathers
+//   ABL_NORING  ABL_NOWLOAD + ABL_NOSCALE: the ring issues no memory operation
+//   ABL_L2WIN   weight loads folded into a 256 KiB window (L2-resident, same instructions)
 #include <hip/hip_runtime.h>
 
+#if defined(ABL_NORING)  // no memory traffic in the ring at all
+#define ABL_NOWLOAD
+#define ABL_NOSCALE
+#endif
 #if defined(ABL_NOLUT)
 #define NF4_ABL_LOOKUP(pt_, addr_, wd_) \
     (f32x2{__uint_as_float(((addr_) & 0xFFFFu) | 0x3F000000u), __uint_as_float(((wd_) & 0xFFFFu) | 0x3E000000u)})
-#elif defined(ABL_NOWLOAD)
+#endif
+#if defined(ABL_NOWLOAD)
 #define NF4_ABL_WLOAD(rsrc_, off_) (u32x4{(off_), (off_) * 3u, (off_) ^ 0x5A5A5A5Au, (off_) + 0x01010101u})
-#elif defined(ABL_NOMMA)
+#elif defined(ABL_L2WIN)  // weight loads folded into a 256 KiB window per weight: L2 hits, same instructions
+#define NF4_ABL_WLOAD(rsrc_, off_) __builtin_amdgcn_raw_buffer_load_b128((rsrc_), (off_) & 0x8003FFF0u, 0, 0)
+#endif
+#if defined(ABL_NOSCALE)  // absmax byte / nested scale from the offset (no gather)
+#define NF4_ABL_SLOAD(rsrc_, off_, b8_) ((b8_) ? (((off_) * 37u) & 0x7Fu) | 1u : 0x3C000000u | ((off_) & 0xFFFFu))
+#endif
+#if defined(ABL_NOX)
+#define NF4_ABL_X_ON 0
+#endif
+#if defined(ABL_NOMMA)
 #define NF4_ABL_MMA_ON 0
 #define NF4_ABL_RED_ON 1
 #define NF4_ABL_HANDOFF_ON 1
