@@ -226,6 +226,23 @@ __device__ __forceinline__ void splitk_reduce(uint64_t* slab, uint32_t ksplit, u
     }
 }
 
+// Two K slices: the hand-off by exchange, one memory round trip.  Both slices
+// swap their pair of partials into the same slab entry (atomic exchange, relaxed,
+// agent scope); exactly one of them gets back 0 (empty) and is done, the other
+// gets back its partner's pair, sums the two in slice order (p0 + p1, bitwise the
+// same as splitk_reduce), writes y and stores 0 so the entry is empty for the next
+// call (ordered by the kernel boundary).  No ticket, no poll.  A partial whose NOT
+// would be 0 (the NaN 0xFFFFFFFF) is sent as the NaN 0x7FFFFFFF, so a written
+// entry is never 0 and the output is a NaN either way.
+__device__ __forceinline__ uint32_t slab_not(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return b == 0xFFFFFFFFu ? 0x80000000u : ~b;
+}
+__device__ __forceinline__ uint64_t slab_swap2(uint64_t* p, float lo, float hi) {
+    const uint64_t w = ((uint64_t)slab_not(hi) << 32) | (uint64_t)slab_not(lo);
+    return __hip_atomic_exchange(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int DT>
 __device__ __forceinline__ void store_y(void* y, uint32_t i, float v) {
     if constexpr (DT == NF4DQ_BF16) {
@@ -1019,6 +1036,50 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
         return;
     }
     if constexpr (!NF4_ABL_HANDOFF_ON) return;
+    if (S == 2) {
+        // two K slices (K <= 4096 at M > 16): hand-off by exchange (slab_swap2) in the
+        // first slice's entries, kB swaps per thread in flight before any result is used
+        constexpr int kB = 4;
+        const uint32_t total = nst * rows * 8u;
+        for (uint32_t e0 = tid; e0 < total; e0 += (uint32_t)kB * 64u * WV) {
+            uint64_t got[kB];
+            float lo[kB], hi[kB];
+            uint32_t ent[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const uint32_t e = e0 + (uint32_t)b * 64u * WV;
+                got[b] = 0;
+                lo[b] = hi[b] = 0.0f;
+                ent[b] = 0;
+                if (e < total) {
+                    const uint32_t t = e / (rows * 8u), rem = e - t * rows * 8u, m = rem >> 3, c = 2u * (rem & 7u);
+                    const float* h = held + t * (16u * MT * 16u) + m * 16u + c;
+                    lo[b] = h[0];
+                    hi[b] = h[1];
+                    ent[b] = slab_entry(0, A.M, m, A.ncols, (s0 + t) * 16u + c);
+                    got[b] = slab_swap2(A.slab + ent[b], lo[b], hi[b]);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                if (got[b] == 0) continue;  // first of the two (or past the end): the partner finishes
+                const uint32_t e = e0 + (uint32_t)b * 64u * WV;
+                const uint32_t t = e / (rows * 8u), rem = e - t * rows * 8u, m = rem >> 3, p = rem & 7u;
+                const float plo = __uint_as_float(~(uint32_t)got[b]), phi = __uint_as_float(~(uint32_t)(got[b] >> 32));
+                const float slo = ks == 0 ? lo[b] + plo : plo + lo[b];  // slice order
+                const float shi = ks == 0 ? hi[b] + phi : phi + hi[b];
+                const uint32_t strip = s0 + t;
+                const K128Mat& Mt = A.mat[xr_mat_of(A, strip)];
+                uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(Mt.y) + m * Mt.N +
+                                                            (strip - Mt.cg_begin) * 16u + 2u * p);
+                *dst = pack2<DT>(slo, shi);
+                __hip_atomic_store(A.slab + ent[b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        NF4_GSTAMP(5);
+        NF4_GSTAMP(9);
+        return;
+    }
     // slab [ks][M][ncols] entries (strip s at columns 16 s): splitk_ticket / splitk_reduce
     for (uint32_t e = tid; e < nst * rows * 8u; e += 64u * WV) {  // column pairs
         const uint32_t t = e / (rows * 8u), rem = e - t * rows * 8u, m = rem >> 3, c = 2u * (rem & 7u);
@@ -1572,6 +1633,52 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     // group a ticket; the slice drawing ksplit - 1 sums all slices in slice order
     // (splitk_ticket / splitk_reduce)
     const float* o32 = reinterpret_cast<const float*>(smem + A.out_off);
+    if (KS == 2) {
+        // two slices: hand-off by exchange (slab_swap2) in the first slice's entries,
+        // kB swaps per thread in flight before any result is used
+        constexpr int kB = 4;
+        for (uint32_t i0 = 2u * tid; i0 < mine * per; i0 += (uint32_t)kB * 2u * 64u * W) {
+            uint64_t got[kB];
+            uint32_t ent[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const uint32_t i = i0 + (uint32_t)b * 2u * 64u * W;
+                got[b] = 0;
+                ent[b] = 0;
+                if (i < mine * per) {
+                    const uint32_t ito = i / per, rem = i - ito * per;
+                    const uint32_t t = rem / (A.M * 16u), rem2 = rem - t * (A.M * 16u);
+                    const uint32_t sgi = j0 + ito * G;
+                    uint32_t mi = 0;
+                    for (uint32_t j = 1; j < A.nmat; ++j) mi = sgi >= A.mat[j].sg_begin ? j : mi;
+                    const uint32_t gstrip = A.mat[mi].strip_begin + (sgi - A.mat[mi].sg_begin) * A.T + t;
+                    ent[b] = slab_entry(0, A.M, rem2 >> 4, A.ncols, gstrip * 16u + (rem2 & 15u));
+                    got[b] = slab_swap2(A.slab + ent[b], o32[i], o32[i + 1]);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                if (got[b] == 0) continue;  // first of the two (or past the end): the partner finishes
+                const uint32_t i = i0 + (uint32_t)b * 2u * 64u * W;
+                const uint32_t ito = i / per, rem = i - ito * per;
+                const uint32_t t = rem / (A.M * 16u), rem2 = rem - t * (A.M * 16u);
+                const uint32_t sgi = j0 + ito * G;
+                uint32_t mi = 0;
+                for (uint32_t j = 1; j < A.nmat; ++j) mi = sgi >= A.mat[j].sg_begin ? j : mi;
+                const StreamMat& Mt = A.mat[mi];
+                const float plo = __uint_as_float(~(uint32_t)got[b]), phi = __uint_as_float(~(uint32_t)(got[b] >> 32));
+                const float slo = ks == 0 ? o32[i] + plo : plo + o32[i];  // slice order
+                const float shi = ks == 0 ? o32[i + 1] + phi : phi + o32[i + 1];
+                const uint32_t col = ((sgi - Mt.sg_begin) * A.T + t) * 16u + (rem2 & 15u);
+                *reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(Mt.y) + (rem2 >> 4) * Mt.N + col) =
+                    pack2<DT>(slo, shi);
+                __hip_atomic_store(A.slab + ent[b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        NF4_GSTAMP(5);
+        NF4_GSTAMP(9);
+        return;
+    }
     for (uint32_t i = 2u * tid; i < mine * per; i += 2u * 64u * W) {  // column pairs
         const uint32_t ito = i / per, rem = i - ito * per;
         const uint32_t t = rem / (A.M * 16u), rem2 = rem - t * (A.M * 16u);

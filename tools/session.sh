@@ -100,6 +100,12 @@ for stage in "$@"; do
             --output-format csv -d "$O/pmcg_b" -o b -- python3 -u $GA > "$O/pmcg_b.log" 2>&1
         python3 tools/pmc_gemm.py "$O" nf4_gemm_xr_kernel nf4_gemm_persist_kernel nf4_gemm_stream_kernel > "$O/pmc_gemm.jsonl"
         cat "$O/pmc_gemm.jsonl" ;;
+    sweep)  # fused-GEMM decomposition sweep: SWEEP_ARGS passed to tools/sweep_gemm.py
+        timeout -k 10 600 $PY tools/sweep_gemm.py ${SWEEP_ARGS:-} > "$O/sweep_gemm.jsonl" 2> "$O/sweep_gemm.err"
+        python3 -c "import json,sys
+for l in open(sys.argv[1]):
+    if l.startswith('{'):
+        d=json.loads(l); print(d['N'], d['K'], d['M'], 'default', d['default_us'], 'best', d['best'][:3])" "$O/sweep_gemm.jsonl" ;;
     gemmpass)  # the Llama-3-8B decode pass, fused GEMM (tools/bench_gemm.py)
         timeout -k 10 500 $PY tools/bench_gemm.py --ms ${GEMM_MS:-1,4,8,12,16,24,32} > "$O/bench_gemm.jsonl" 2> "$O/bench_gemm.err"
         cat "$O/bench_gemm.jsonl" ;;

@@ -78,7 +78,8 @@ def main():
             for waves in (4, 8, 16):
                 for depth in (2, 4):
                     for strips in (1, 2, 4):
-                        cfgs.append(_lib.GemmCfg(_lib.GEMM_PERSIST, waves, depth, 1, strips))
+                        for ks in (1, 2, 4):
+                            cfgs.append(_lib.GemmCfg(_lib.GEMM_PERSIST, waves, depth, ks, strips))
             for waves in (4, 8, 16):
                 for depth in (2, 4, 8):
                     for strips in (1, 2, 4):
