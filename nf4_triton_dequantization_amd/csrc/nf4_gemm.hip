@@ -238,6 +238,13 @@ __device__ __forceinline__ uint32_t slab_not(float f) {
     const uint32_t b = __float_as_uint(f);
     return b == 0xFFFFFFFFu ? 0x80000000u : ~b;
 }
+// Exchange entries are laid out [strip][row][column pair] (a strip's M x 8 pairs
+// contiguous), so consecutive lanes of the exchange loops hit consecutive 8-byte
+// entries: 512 contiguous bytes per wave instruction instead of 64-byte pieces of
+// eight rows.  Same footprint as one slice of the [ks][M][ncols / 2] slab.
+__device__ __forceinline__ uint32_t swap_entry(uint32_t strip, uint32_t M, uint32_t m, uint32_t col) {
+    return (strip * M + m) * 8u + (col >> 1);
+}
 __device__ __forceinline__ uint64_t slab_swap2(uint64_t* p, float lo, float hi) {
     const uint64_t w = ((uint64_t)slab_not(hi) << 32) | (uint64_t)slab_not(lo);
     return __hip_atomic_exchange(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1056,7 +1063,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
                     const float* h = held + t * (16u * MT * 16u) + m * 16u + c;
                     lo[b] = h[0];
                     hi[b] = h[1];
-                    ent[b] = slab_entry(0, A.M, m, A.ncols, (s0 + t) * 16u + c);
+                    ent[b] = swap_entry(s0 + t, A.M, m, c);
                     got[b] = slab_swap2(A.slab + ent[b], lo[b], hi[b]);
                 }
             }
@@ -1652,7 +1659,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
                     uint32_t mi = 0;
                     for (uint32_t j = 1; j < A.nmat; ++j) mi = sgi >= A.mat[j].sg_begin ? j : mi;
                     const uint32_t gstrip = A.mat[mi].strip_begin + (sgi - A.mat[mi].sg_begin) * A.T + t;
-                    ent[b] = slab_entry(0, A.M, rem2 >> 4, A.ncols, gstrip * 16u + (rem2 & 15u));
+                    ent[b] = swap_entry(gstrip, A.M, rem2 >> 4, rem2 & 15u);
                     got[b] = slab_swap2(A.slab + ent[b], o32[i], o32[i + 1]);
                 }
             }
