@@ -79,7 +79,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_HBM = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
-ROUNDS = ("r02", "r01")  # profiles/<round>/pmc_traffic.json, newest first
+ROUNDS = ("r03", "r02", "r01")  # profiles/<round>/pmc_traffic.json, newest first
 # bytes of buffer sets per rank: 2x the 256 MiB Infinity Cache.  The per-launch time is
 # flat from ~300 MB to ~1.1 GB of rotating sets (the HBM-streaming regime: 4096^2 6.93-6.95
 # us at 7..26 sets), lower below it (Infinity Cache hits: 6.39 us at 2 sets) and ~5-10 %
