@@ -814,8 +814,8 @@ __device__ __forceinline__ void xr_pair_mma(const u32x4& w0, const u32x4& w1, fl
 // 4-11 of the next) the 16 lanes then hit 16 distinct 4-bank sets.
 __device__ __forceinline__ uint32_t xr_xsw(uint32_t r) { return r ^ ((((r + 4u) >> 3) & 1u) << 3); }
 
-template <int DT, int MT, int WV, int KPW, int D>
-__global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) {
+template <int DT, int MT, int WV, int KPW, int D, int GU>
+__device__ __forceinline__ void xr_body(const GemmArgs& A) {
     extern __shared__ __attribute__((aligned(16))) f32x4 xr_smem[];  // dynamic part (host: xr_lds_dynamic)
     // 256-deep chunks: the pair table (64 KiB) and the q/127 table, static so that the
     // lookups' addresses need no base added (one VALU per two weights less than in a
@@ -826,6 +826,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     float* qtab = xr_qtab;
     // partial tiles meet once per R strips (8 waves: two strips per barrier)
     constexpr int R = WV == 8 && D % 2 == 0 ? 2 : 1;
+    static_assert(GU == 0 || (R * MT <= WV && D == R), "unrolled groups: one tile per wave and group");
     f32x4* red = xr_smem;                                    // [2][R][WV][MT][64] partial tiles
     float* lut = reinterpret_cast<float*>(red + 2 * R * WV * MT * 64);  // 16 codes
     uint32_t* last_flags = reinterpret_cast<uint32_t*>(lut + 16);        // [64] split-K tickets drawn last
@@ -940,7 +941,18 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
     // Every unrolled step issues its refill, past the last strip too (out of range:
     // no traffic): with a `break` the loop latch would also be reached right after
     // step 0's refill, and the waits at the loop head would drain the ring.
-    for (uint32_t t0 = 0; t0 < nst; t0 += (uint32_t)D) {
+    // One reduction group (D = R strips, or D strips in R-sized groups) per call.
+    // GU > 0 (two K slices, at most GU groups per workgroup): the groups are unrolled
+    // so that each one's exchange results land in registers of their own (gotg[gi]),
+    // and the reducer wave exchanges a group's sums as soon as they are summed: the
+    // exchanges' traffic overlaps the next groups' dequant + MFMA instead of
+    // following the last strip.
+    uint64_t gotg[GU > 0 ? GU : 1][4];
+#pragma unroll
+    for (int gi = 0; gi < (GU > 0 ? GU : 1); ++gi)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gotg[gi][q] = 0;
+    auto group = [&](uint32_t t0, uint64_t (&gg)[4]) __attribute__((always_inline)) {
         f32x4 accs[R][MT];  // the partials of the current reduction group (R strips)
 #pragma unroll
         for (int d = 0; d < D; ++d) {
@@ -1001,6 +1013,31 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
                 __syncthreads();
                 NF4_GSPAN_END(7);  // partial tiles stored + the barrier
                 NF4_GSPAN_BEGIN();
+                if constexpr (GU > 0) {
+                    // the one tile of the group this wave reduces (tile j = r MT + mt goes
+                    // to wave (tg MT + j) mod WV, as below), with a single exchange site
+                    // per result register: a merge of several sites made the compiler
+                    // move the pending results between registers (a vmcnt(0) per move)
+                    const uint32_t j = (wave + (uint32_t)WV - (tg * (uint32_t)MT) % (uint32_t)WV) % (uint32_t)WV;
+                    const uint32_t r = j / (uint32_t)MT, mt = j % (uint32_t)MT, u = tg + r;
+                    if (j < (uint32_t)(R * MT) && u < nst) {  // uniform
+                        const f32x4* rb = red + (((u / R) & 1u) * R + r) * (WV * MT * 64);
+                        f32x4 sum = rb[mt * 64 + lane];
+#pragma unroll
+                        for (int w = 1; w < WV; ++w) sum += rb[(w * MT + mt) * 64 + lane];
+                        float* h = held + u * (16u * MT * 16u) + (16u * mt + 4u * kh) * 16u + nl;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            h[16u * q] = sum[q];
+                            const float nb = __shfl_xor(sum[q], 1, 64);
+                            const uint32_t m = 16u * mt + 4u * kh + q;
+                            if (m < A.M && !(nl & 1u))
+                                gg[q] = slab_swap2(A.slab + swap_entry(s0 + u, A.M, m, nl), sum[q], nb);
+                        }
+                    }
+                    NF4_GSPAN_END(8);
+                    continue;
+                }
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t u = tg + (uint32_t)r;
@@ -1021,6 +1058,46 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
                 NF4_GSPAN_END(8);  // the reducer's sums
             }
         }
+    };
+    if constexpr (GU > 0) {
+#pragma unroll
+        for (int gi = 0; gi < GU; ++gi)
+            if ((uint32_t)gi * (uint32_t)D < nst) group((uint32_t)gi * (uint32_t)D, gotg[gi]);  // uniform
+    } else {
+        for (uint32_t t0 = 0; t0 < nst; t0 += (uint32_t)D) group(t0, gotg[0]);
+    }
+    if constexpr (GU > 0) {
+        // each reducer wave finishes its own tiles' exchanges: the second arriver sums
+        // in slice order (its sums in `held`, written by this wave) and writes y
+#pragma unroll
+        for (int gi = 0; gi < GU; ++gi) {
+            const uint32_t tg = (uint32_t)gi * (uint32_t)D;
+            const uint32_t j = (wave + (uint32_t)WV - (tg * (uint32_t)MT) % (uint32_t)WV) % (uint32_t)WV;
+            const uint32_t r = j / (uint32_t)MT, mt = j % (uint32_t)MT, u = tg + r;
+            if (j >= (uint32_t)(R * MT) || u >= nst) continue;  // uniform: no tile of this wave
+            {
+                const uint32_t strip = s0 + u;
+                const uint32_t mi = __builtin_amdgcn_readfirstlane(xr_mat_of(A, strip));
+                uint16_t* const ybase = reinterpret_cast<uint16_t*>(A.mat[mi].y);
+                const uint32_t yN = A.mat[mi].N, ycol = (strip - A.mat[mi].cg_begin) * 16u;
+                {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint64_t g = gotg[gi][q];
+                        if (g == 0) continue;  // not sent, or the first of the two
+                        const uint32_t m = 16u * mt + 4u * kh + q;
+                        const float* h = held + u * (16u * MT * 16u) + m * 16u + nl;
+                        const float plo = __uint_as_float(~(uint32_t)g), phi = __uint_as_float(~(uint32_t)(g >> 32));
+                        const float slo = ks == 0 ? h[0] + plo : plo + h[0];  // slice order
+                        const float shi = ks == 0 ? h[1] + phi : phi + h[1];
+                        *reinterpret_cast<uint32_t*>(ybase + m * yN + ycol + nl) = pack2<DT>(slo, shi);
+                        __hip_atomic_store(A.slab + swap_entry(strip, A.M, m, nl), 0ull, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+        }
+        return;
     }
     NF4_GSTAMP(3);
     __syncthreads();
@@ -1109,6 +1186,20 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) 
         splitk_reduce<DT, 16u>(A.slab, S, A.M, A.ncols, strip * 16u, Mt.y, Mt.N, lc, lane);
     }
     NF4_GSTAMP(9);
+}
+
+template <int DT, int MT, int WV, int KPW, int D, int GU>
+__global__ __launch_bounds__(64 * WV) void nf4_gemm_xr_kernel(const GemmArgs A) {
+    xr_body<DT, MT, WV, KPW, D, GU>(A);
+}
+// GU > 0: the unrolled groups keep 4 x 4 exchange results per lane live across the
+// loop; at one workgroup of 8 waves per CU (2 per SIMD) the kernel may use up to
+// 256 registers, and with the default budget the allocator moved those results
+// between registers (each move a full vmcnt(0) drain inside the ring)
+template <int DT, int MT, int WV, int KPW, int D, int GU>
+__global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(1, 2))) void nf4_gemm_xrg_kernel(
+    const GemmArgs A) {
+    xr_body<DT, MT, WV, KPW, D, GU>(A);
 }
 
 // ---------------------------------------------------------------------------
@@ -2261,16 +2352,29 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
     const uint32_t groups = (strips + A.per_wg - 1) / A.per_wg;
     const dim3 grid(groups * ks), block(64 * cfg.waves);
     const uint32_t lds = xr_lds_dynamic(M, cfg.waves, A.per_wg);
-#define NF4_R1(DT_, MT_, W_, KPW_, D_)                                                                               \
+#define NF4_R2(DT_, MT_, W_, KPW_, D_, GU_)                                                                          \
     do {                                                                                                             \
         static bool attr_ = false; /* dynamic LDS above 64 KiB needs the opt-in */                                   \
         if (!attr_) {                                                                                                \
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_xr_kernel<DT_, MT_, W_, KPW_, D_>),    \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,                                    \
-                                      (int)(kLdsPerCu - xr_lds_static(KPW_)));                                       \
+            (void)hipFuncSetAttribute(                                                                               \
+                GU_ ? reinterpret_cast<const void*>(&nf4_gemm_xrg_kernel<DT_, MT_, W_, KPW_, D_, GU_>)               \
+                    : reinterpret_cast<const void*>(&nf4_gemm_xr_kernel<DT_, MT_, W_, KPW_, D_, GU_>),               \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsPerCu - xr_lds_static(KPW_)));                 \
             attr_ = true;                                                                                            \
         }                                                                                                            \
-        hipLaunchKernelGGL((nf4_gemm_xr_kernel<DT_, MT_, W_, KPW_, D_>), grid, block, lds, st, A);                   \
+        if (GU_) hipLaunchKernelGGL((nf4_gemm_xrg_kernel<DT_, MT_, W_, KPW_, D_, GU_>), grid, block, lds, st, A);    \
+        else hipLaunchKernelGGL((nf4_gemm_xr_kernel<DT_, MT_, W_, KPW_, D_, GU_>), grid, block, lds, st, A);         \
+    } while (0)
+    // two K slices of 8 waves x 256-deep chunks with at most 4 reduction groups (8
+    // strips) per workgroup: the groups unrolled, exchanges issued inside the loop
+#define NF4_R1(DT_, MT_, W_, KPW_, D_)                                                   \
+    do {                                                                                 \
+        if constexpr (W_ == 8 && KPW_ == 2 && D_ == 2) {                                 \
+            if (ks == 2 && A.per_wg <= 8) NF4_R2(DT_, MT_, W_, KPW_, D_, 4);             \
+            else NF4_R2(DT_, MT_, W_, KPW_, D_, 0);                                      \
+        } else {                                                                         \
+            NF4_R2(DT_, MT_, W_, KPW_, D_, 0);                                           \
+        }                                                                                \
     } while (0)
 #define NF4_RD(DT_, MT_, W_, KPW_)                         \
     do {                                                   \
@@ -2300,6 +2404,7 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
 #undef NF4_RK
 #undef NF4_RD
 #undef NF4_R1
+#undef NF4_R2
     return hip_rc2(hipGetLastError());
 }
 

@@ -214,12 +214,15 @@ def test_every_decomposition_agrees_with_oracle(coracle, gpu, dt, M, N, K):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
-@pytest.mark.parametrize("M,K,kpw", [(32, 4096, 2), (17, 4096, 2), (32, 2048, 1), (24, 4096, 4)])
-def test_xr_multi_strip_workgroups(coracle, gpu, dt, M, K, kpw):
+@pytest.mark.parametrize("M,K,kpw,spw", [(32, 4096, 2, 3), (32, 4096, 2, 9), (17, 4096, 2, 3), (32, 2048, 1, 3),
+                                         (24, 4096, 4, 3)])
+def test_xr_multi_strip_workgroups(coracle, gpu, dt, M, K, kpw, spw):
     """The register-resident kernel with several 16-column strips per workgroup, at
-    any CU count: N is sized from the device's CUs so that every workgroup walks >= 3
+    any CU count: N is sized from the device's CUs so that every workgroup walks >= spw
     strips (its ring refills, partial-tile reduction groups and cached weight
-    descriptors all cross strip boundaries)."""
+    descriptors all cross strip boundaries).  At two K slices, spw = 3 takes the
+    unrolled-group form (exchanges inside the strip loop, <= 8 strips per workgroup)
+    and spw = 9 the looped form (exchanges after it)."""
     from nf4_triton_dequantization_amd import _lib
 
     L = _lib.lib()
@@ -228,9 +231,9 @@ def test_xr_multi_strip_workgroups(coracle, gpu, dt, M, K, kpw):
     ks = -(-(K // 128) // (waves * kpw))
     # the library's grid (xr_per_wg): one workgroup per CU, two for 128-deep chunks
     wg_per_slice = max(1, cus * (2 if kpw == 1 else 1) // ks)
-    N = 16 * 3 * wg_per_slice         # >= 3 strips per workgroup
+    N = 16 * spw * wg_per_slice       # >= spw strips per workgroup
     N = -(-N // 64) * 64
-    assert (N // 16) / wg_per_slice >= 3
+    assert (N // 16) / wg_per_slice >= spw
     packed, a1, a2 = O.make_inputs(N, K, seed=N + K + M + kpw, a2_kind="normal")
     W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16)
     t = (torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu))
