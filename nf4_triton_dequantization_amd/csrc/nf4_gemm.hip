@@ -2365,12 +2365,13 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
         if (GU_) hipLaunchKernelGGL((nf4_gemm_xrg_kernel<DT_, MT_, W_, KPW_, D_, GU_>), grid, block, lds, st, A);    \
         else hipLaunchKernelGGL((nf4_gemm_xr_kernel<DT_, MT_, W_, KPW_, D_, GU_>), grid, block, lds, st, A);         \
     } while (0)
-    // two K slices of 8 waves x 256-deep chunks with at most 4 reduction groups (8
-    // strips) per workgroup: the groups unrolled, exchanges issued inside the loop
+    // two K slices of 8 waves x 256-deep chunks with at most 4 or 8 reduction groups
+    // (8 or 16 strips) per workgroup: the groups unrolled, exchanges issued inside the loop
 #define NF4_R1(DT_, MT_, W_, KPW_, D_)                                                   \
     do {                                                                                 \
         if constexpr (W_ == 8 && KPW_ == 2 && D_ == 2) {                                 \
             if (ks == 2 && A.per_wg <= 8) NF4_R2(DT_, MT_, W_, KPW_, D_, 4);             \
+            else if (ks == 2 && A.per_wg <= 16) NF4_R2(DT_, MT_, W_, KPW_, D_, 8);       \
             else NF4_R2(DT_, MT_, W_, KPW_, D_, 0);                                      \
         } else {                                                                         \
             NF4_R2(DT_, MT_, W_, KPW_, D_, 0);                                           \
