@@ -98,7 +98,7 @@ for stage in "$@"; do
         timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INST_LEVEL_VMEM \
             SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_VMEM_TA_ADDR_FIFO_FULL \
             --output-format csv -d "$O/pmcg_b" -o b -- python3 -u $GA > "$O/pmcg_b.log" 2>&1
-        python3 tools/pmc_gemm.py "$O" nf4_gemm_xr_kernel nf4_gemm_persist_kernel nf4_gemm_stream_kernel > "$O/pmc_gemm.jsonl"
+        python3 tools/pmc_gemm.py "$O" nf4_gemm_xrg_kernel nf4_gemm_xr_kernel nf4_gemm_persist_kernel nf4_gemm_stream_kernel > "$O/pmc_gemm.jsonl"
         cat "$O/pmc_gemm.jsonl" ;;
     sweep)  # fused-GEMM decomposition sweep: SWEEP_ARGS passed to tools/sweep_gemm.py
         timeout -k 10 600 $PY tools/sweep_gemm.py ${SWEEP_ARGS:-} > "$O/sweep_gemm.jsonl" 2> "$O/sweep_gemm.err"
