@@ -116,7 +116,7 @@ def parse_args(argv=None):
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--nontemporal", type=int, default=1)
     ap.add_argument("--flags", type=lambda v: int(v, 0), default=0,
-                    help="nf4_launch_cfg.flags: (log2 absmax prefetch distance in tiles) << 8, 0 = off")
+                    help="nf4_launch_cfg.flags: reserved, must be 0 (the library rejects anything else)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])

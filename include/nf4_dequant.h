@@ -42,6 +42,7 @@ extern "C" {
 #define NF4DQ_ERR_ARG 1        /* null pointer, bad dtype, negative size      */
 #define NF4DQ_ERR_SHAPE 2      /* sizes the reference would reject (view fails) */
 #define NF4DQ_ERR_TOO_LARGE 3  /* a single matrix beyond 2^31 packed bytes    */
+#define NF4DQ_ERR_SPLITK_TIMEOUT 4 /* nf4_gemm_check_workspace: a split-K reducer gave up */
 #define NF4DQ_ERR_HIP_BASE 1000
 
 /* Reference double dequant of one Linear4bit weight into row-major out[m][n].
@@ -181,6 +182,13 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
  * only, K % 512 == 0); ksplit must equal ceil(K/128 / (waves * strips))
  * (1 = no cross-workgroup reduction). */
 #define NF4DQ_GEMM_XR 5
+/* NF4DQ_GEMM_SK: balanced ("stream-K") kernel (K % 256 == 0, M K 2 <= 64 KiB):
+ * one workgroup of `waves` (16) waves per CU, the (16-column strip, 256-deep
+ * chunk) units of the launch split evenly over the waves, x[M][K] in LDS;
+ * strips shared by neighbouring workgroups meet in the split-K slab.  depth and
+ * strips are ignored, ksplit must be 1.  Needs at least one unit per CU and at
+ * most one strip (and 16 units) per wave, else NF4DQ_ERR_ARG. */
+#define NF4DQ_GEMM_SK 6
 typedef struct nf4_gemm_cfg {
     int32_t kernel;
     int32_t waves;
@@ -218,6 +226,15 @@ size_t nf4_gemm_grouped_workspace_bytes(int64_t M, int64_t K, const nf4_gemm_mat
 int nf4_gemm_ref_grouped(const void* x, int64_t M, int64_t K, const nf4_gemm_mat* mats, int32_t count,
                          int32_t out_dtype, void* workspace, size_t workspace_bytes,
                          const nf4_gemm_cfg* cfg, void* hip_stream);
+
+/* The split-K hand-off never hangs: a reducer that has polled a partner slice's
+ * entries 2^16 times without seeing them gives up, reads them as NaN and sets a
+ * sticky error word in the workspace header.  This call waits for `hip_stream`,
+ * reads that word and returns NF4DQ_OK, or NF4DQ_ERR_SPLITK_TIMEOUT after
+ * zero-filling the whole workspace again (a stalled slice's late entries
+ * included), so it is reusable.  NULL / 0-byte workspace: NF4DQ_OK (no split-K,
+ * nothing to report).  Synchronous; call it after the calls it vouches for. */
+int nf4_gemm_check_workspace(void* workspace, size_t workspace_bytes, void* hip_stream);
 
 /* Human-readable text for a return code (static storage). */
 const char* nf4_strerror(int code);

@@ -29,6 +29,7 @@ OK = 0
 ERR_ARG = 1
 ERR_SHAPE = 2
 ERR_TOO_LARGE = 3
+ERR_SPLITK_TIMEOUT = 4
 ERR_HIP_BASE = 1000
 
 BATCH_MAX = 24
@@ -67,6 +68,7 @@ GEMM_STREAM = 2
 GEMM_PERSIST = 3
 GEMM_XS = 4
 GEMM_XR = 5
+GEMM_SK = 6
 
 
 GEMM_GROUP_MAX = 8
@@ -109,6 +111,7 @@ SIGNATURES = {
                                                            ctypes.POINTER(GemmCfg)]),
     "nf4_gemm_ref_grouped": (ctypes.c_int, [_P, _I64, _I64, ctypes.POINTER(GemmMat), _I32, _I32, _P, ctypes.c_size_t,
                                             ctypes.POINTER(GemmCfg), _P]),
+    "nf4_gemm_check_workspace": (ctypes.c_int, [_P, ctypes.c_size_t, _P]),
     "nf4_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "nf4_version": (ctypes.c_char_p, []),
 }

@@ -776,6 +776,8 @@ const char* nf4_strerror(int code) {
         case NF4DQ_ERR_ARG: return "invalid argument (null pointer, dtype or negative size)";
         case NF4DQ_ERR_SHAPE: return "shape mismatch (packed weight / absmax cannot be viewed as the reference does)";
         case NF4DQ_ERR_TOO_LARGE: return "matrix too large for one launch";
+        case NF4DQ_ERR_SPLITK_TIMEOUT:
+            return "fused GEMM split-K hand-off timed out (some outputs are NaN; workspace re-zeroed)";
         default: break;
     }
     if (code >= NF4DQ_ERR_HIP_BASE) return hipGetErrorString((hipError_t)(code - NF4DQ_ERR_HIP_BASE));

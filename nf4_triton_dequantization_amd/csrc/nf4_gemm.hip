@@ -9,7 +9,7 @@
 // once (0.5 B/element) and dequantized in registers -- the roofline is HBM on
 // the packed weight, not on a 2 B/element bf16 copy.
 //
-// Five kernels (host choice in default_gemm_cfg, explicit in nf4_gemm_ref_cfg):
+// Six kernels (host choice in default_gemm_cfg, explicit in nf4_gemm_ref_cfg):
 //  * nf4_gemm_smallm_kernel -- K % 128 == 0; 128-deep chunks, a lane loads 16
 //    packed bytes of its weight row (one 64-block, one scale) and the matching
 //    activation fragments from global memory; waves of a workgroup split K and
@@ -19,6 +19,9 @@
 //  * nf4_gemm_xr_kernel -- register-resident x (16 < M <= 32, K % 256 == 0):
 //    each wave holds its K chunk's x fragments for the whole launch and walks
 //    the workgroup's column strips with a register ring of weight chunks.
+//  * nf4_gemm_xrg_kernel -- the same body with the reduction groups unrolled
+//    (two K slices, <= 16 strips per workgroup): each group's split-K exchanges
+//    go out inside the strip loop (up to 2 waves per SIMD, 256 registers).
 //  * nf4_gemm_stream_kernel -- K % 256 == 0 (every Llama shape); 256-deep
 //    chunks (one 128-byte line per weight row), activations staged in LDS,
 //    a register ring of weight chunks, pair-table dequant (see its comments).
@@ -83,6 +86,17 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 #ifndef NF4_ABL_WLOAD
 #define NF4_ABL_WLOAD(rsrc_, off_) __builtin_amdgcn_raw_buffer_load_b128((rsrc_), (off_), 0, 0)
 #endif
+//   NF4_ABL_KEEP_SLICE(ks)        128-deep kernel: K slice ks stores its split-K partials
+//                                 (tools' drop-slice build withholds one slice's: the
+//                                 reducer's poll then gives up and sets the error word)
+//   NF4_ABL_RING_FULL             0 when the ring issues fewer than 4 loads per slot (the
+//                                 staged-x wait then counts nothing)
+#ifndef NF4_ABL_RING_FULL
+#define NF4_ABL_RING_FULL 1
+#endif
+#ifndef NF4_ABL_KEEP_SLICE
+#define NF4_ABL_KEEP_SLICE(ks_) true
+#endif
 #ifndef NF4_ABL_MMA_ON
 #define NF4_ABL_MMA_ON 1
 #define NF4_ABL_RED_ON 1
@@ -102,13 +116,23 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 // previous call's reader cleared it, ordered by the kernel boundary), sums them
 // in slice order (bitwise reproducible) and clears them for the next call.  The
 // reader waits only on slices that already drew their tickets, i.e. are running
-// or done, so the wait ends; it is bounded anyway (kSpinMax polls, then NaN: a
-// wrong result, never a hung GPU -- also the outcome, correctly, of a partial that
-// is the one NaN whose NOT is 0).
+// or done, so the wait ends; it is bounded anyway: after kSpinMax polls the
+// missing partials read as NaN AND the workspace's sticky error word (kErrWord,
+// after the counters) is set, so the host learns of it (nf4_gemm_check_workspace)
+// instead of finding NaNs nobody reported -- never a hung GPU, never a silent one.
 constexpr int kSpinMax = 1 << 16;
+constexpr uint32_t kErrWord = 16384;  // uint32 index in the workspace header (byte 64 KiB)
+
+// A partial's bits on the wire: its NOT, except that the one NaN whose NOT would be
+// 0 (0xFFFFFFFF) goes as the NaN 0x7FFFFFFF -- so a written half is never 0 and a
+// reader never mistakes a written entry for an empty one.
+__device__ __forceinline__ uint32_t slab_not(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return b == 0xFFFFFFFFu ? 0x80000000u : ~b;
+}
 
 __device__ __forceinline__ void slab_put2(uint64_t* slab, uint32_t e, float lo, float hi) {
-    const uint64_t w = ((uint64_t)~__float_as_uint(hi) << 32) | (uint64_t)~__float_as_uint(lo);
+    const uint64_t w = ((uint64_t)slab_not(hi) << 32) | (uint64_t)slab_not(lo);
     __hip_atomic_store(slab + e, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -128,11 +152,12 @@ __device__ __forceinline__ void slab_put_lane(uint64_t* slab, uint32_t e, float 
 
 // Poll the entries of v[][] that are not written yet, all of them per round (one
 // memory round trip per round, not one per entry), at most kSpinMax rounds; an
-// entry still empty then reads as the NOT of two NaNs (a wrong result, never a
-// hung GPU).  Entries not to read are ~0 (full) on entry.
+// entry still empty then reads as the NOT of two NaNs and the lane sets the sticky
+// error word *err (a reported wrong result, never a hung GPU).  Entries not to
+// read are ~0 (full) on entry.
 template <int KK, int KU>
 __device__ __forceinline__ void splitk_poll(uint64_t* slab, uint32_t sstride, uint32_t k0, const uint32_t (&idx)[KU],
-                                            uint64_t (&v)[KK][KU]) {
+                                            uint64_t (&v)[KK][KU], uint32_t* err) {
     for (int tries = 0; tries < kSpinMax; ++tries) {
         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
@@ -153,7 +178,10 @@ __device__ __forceinline__ void splitk_poll(uint64_t* slab, uint32_t sstride, ui
     for (int j = 0; j < KK; ++j)
 #pragma unroll
         for (int u = 0; u < KU; ++u)
-            if (!slab_full(v[j][u])) v[j][u] = 0x803FFFFF803FFFFFull;  // NOT of two NaNs
+            if (!slab_full(v[j][u])) {
+                v[j][u] = 0x803FFFFF803FFFFFull;  // NOT of two NaNs
+                __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // vector atomic
+            }
 }
 
 __device__ __forceinline__ bool splitk_ticket(uint32_t* ctr, uint32_t ksplit) {
@@ -170,7 +198,8 @@ __device__ __forceinline__ bool splitk_ticket(uint32_t* ctr, uint32_t ksplit) {
 // (L2-missing), so waiting per entry would serialise them.
 template <int DT, uint32_t KCOLS>
 __device__ __forceinline__ void splitk_reduce(uint64_t* slab, uint32_t ksplit, uint32_t M, uint32_t ncols,
-                                              uint32_t col0, void* y, uint32_t yld, uint32_t ycol0, uint32_t lane) {
+                                              uint32_t col0, void* y, uint32_t yld, uint32_t ycol0, uint32_t lane,
+                                              uint32_t* counters) {
     constexpr uint32_t KP = KCOLS / 2;  // entries per row of the group
     constexpr int kU = 4, kK = 4;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -198,7 +227,7 @@ __device__ __forceinline__ void splitk_reduce(uint64_t* slab, uint32_t ksplit, u
                                    : ~0ull;
                     ok = ok && slab_full(v[j][u]);
                 }
-            if (!__all(ok)) splitk_poll<kK, kU>(slab, sstride, k0, idx, v);  // entries not written yet
+            if (!__all(ok)) splitk_poll<kK, kU>(slab, sstride, k0, idx, v, counters + kErrWord);  // not written yet
 #pragma unroll
             for (int j = 0; j < kK; ++j) {
                 if (k0 + j >= ksplit) break;  // uniform
@@ -231,13 +260,8 @@ __device__ __forceinline__ void splitk_reduce(uint64_t* slab, uint32_t ksplit, u
 // agent scope); exactly one of them gets back 0 (empty) and is done, the other
 // gets back its partner's pair, sums the two in slice order (p0 + p1, bitwise the
 // same as splitk_reduce), writes y and stores 0 so the entry is empty for the next
-// call (ordered by the kernel boundary).  No ticket, no poll.  A partial whose NOT
-// would be 0 (the NaN 0xFFFFFFFF) is sent as the NaN 0x7FFFFFFF, so a written
-// entry is never 0 and the output is a NaN either way.
-__device__ __forceinline__ uint32_t slab_not(float f) {
-    const uint32_t b = __float_as_uint(f);
-    return b == 0xFFFFFFFFu ? 0x80000000u : ~b;
-}
+// call (ordered by the kernel boundary).  No ticket, no poll.  Partials go through
+// slab_not as in slab_put2, so a written entry is never 0.
 // Exchange entries are laid out [strip][row][column pair] (a strip's M x 8 pairs
 // contiguous), so consecutive lanes of the exchange loops hit consecutive 8-byte
 // entries: 512 contiguous bytes per wave instruction instead of 64-byte pieces of
@@ -477,6 +501,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     // (splitk_ticket / splitk_reduce); the workgroup drawing ksplit-1 sums all
     // slices in slice order and writes y.  Bitwise reproducible.
     const uint32_t scol = Mt.col_begin + row;  // slab column of this lane (strip 0)
+    if (NF4_ABL_KEEP_SLICE(ks))
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -492,7 +517,7 @@ __global__ __launch_bounds__(64 * WV) void nf4_gemm_smallm_kernel(const GemmArgs
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
     splitk_reduce<DT, 16u * NT>(A.slab, A.ksplit, A.M, A.ncols, Mt.col_begin + cgl * 16u * NT, Mt.y, Mt.N,
-                                cgl * 16u * NT, lane);
+                                cgl * 16u * NT, lane, A.counters);
 }
 
 // ---------------------------------------------------------------------------
@@ -639,7 +664,7 @@ __global__ __launch_bounds__(64 * WV, 4) void nf4_gemm_xs_kernel(const GemmArgs 
     if (lane == 0) last = splitk_ticket(&A.counters[ctr], A.ksplit);
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
-    splitk_reduce<DT, 16u>(A.slab, A.ksplit, A.M, A.ncols, Mt.col_begin + strip * 16u, Mt.y, Mt.N, strip * 16u, lane);
+    splitk_reduce<DT, 16u>(A.slab, A.ksplit, A.M, A.ncols, Mt.col_begin + strip * 16u, Mt.y, Mt.N, strip * 16u, lane, A.counters);
 }
 
 // ---------------------------------------------------------------------------
@@ -907,8 +932,10 @@ __device__ __forceinline__ void xr_body(const GemmArgs& A) {
     NF4_GSTAMP(10);
     if constexpr (kStage) {
         // the x DMA went out before the ring's D x 4 loads: wait for it alone (the
-        // compiler does not order LDS-DMA writes before these LDS reads by itself)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * D) : "memory");
+        // compiler does not order LDS-DMA writes before these LDS reads by itself);
+        // an ablation build whose ring issues fewer loads waits for everything
+        if constexpr (NF4_ABL_RING_FULL) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * D) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // fragment (q, s) of row tile mt = piece 8 kh + 4 q + s of row 16 mt + nl
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
@@ -1031,7 +1058,7 @@ __device__ __forceinline__ void xr_body(const GemmArgs& A) {
                             h[16u * q] = sum[q];
                             const float nb = __shfl_xor(sum[q], 1, 64);
                             const uint32_t m = 16u * mt + 4u * kh + q;
-                            if (m < A.M && !(nl & 1u))
+                            if (NF4_ABL_HANDOFF_ON && m < A.M && !(nl & 1u))
                                 gg[q] = slab_swap2(A.slab + swap_entry(s0 + u, A.M, m, nl), sum[q], nb);
                         }
                     }
@@ -1066,6 +1093,7 @@ __device__ __forceinline__ void xr_body(const GemmArgs& A) {
     } else {
         for (uint32_t t0 = 0; t0 < nst; t0 += (uint32_t)D) group(t0, gotg[0]);
     }
+    if constexpr (GU > 0 && !NF4_ABL_HANDOFF_ON) return;
     if constexpr (GU > 0) {
         // each reducer wave finishes its own tiles' exchanges: the second arriver sums
         // in slice order (its sums in `held`, written by this wave) and writes y
@@ -1183,7 +1211,7 @@ __device__ __forceinline__ void xr_body(const GemmArgs& A) {
         const K128Mat& Mt = A.mat[xr_mat_of(A, strip)];
         const uint32_t lc = (strip - Mt.cg_begin) * 16u;
         NF4_GSTAMP(6);  // tickets drawn: this wave reduces (the last arriver)
-        splitk_reduce<DT, 16u>(A.slab, S, A.M, A.ncols, strip * 16u, Mt.y, Mt.N, lc, lane);
+        splitk_reduce<DT, 16u>(A.slab, S, A.M, A.ncols, strip * 16u, Mt.y, Mt.N, lc, lane, A.counters);
     }
     NF4_GSTAMP(9);
 }
@@ -1524,7 +1552,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     if (lane == 0) last = splitk_ticket(&A.counters[gstrip], A.ksplit);
     last = __builtin_amdgcn_readfirstlane(last);
     if (!last) return;
-    splitk_reduce<DT, 16u>(A.slab, A.ksplit, A.M, A.ncols, gstrip * 16u, Mt.y, Mt.N, strip * 16u, lane);
+    splitk_reduce<DT, 16u>(A.slab, A.ksplit, A.M, A.ncols, gstrip * 16u, Mt.y, Mt.N, strip * 16u, lane, A.counters);
 }
 
 
@@ -1800,13 +1828,214 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         const StreamMat& Mt = A.mat[mi];
         const uint32_t s0 = (sgi - Mt.sg_begin) * A.T;  // first strip of the group within the weight
         const uint32_t col0 = (Mt.strip_begin + s0) * 16u;
-        if (A.T == 4) splitk_reduce<DT, 64u>(A.slab, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
-        else if (A.T == 2) splitk_reduce<DT, 32u>(A.slab, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
-        else splitk_reduce<DT, 16u>(A.slab, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane);
+        if (A.T == 4) splitk_reduce<DT, 64u>(A.slab, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane, A.counters);
+        else if (A.T == 2) splitk_reduce<DT, 32u>(A.slab, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane, A.counters);
+        else splitk_reduce<DT, 16u>(A.slab, KS, A.M, A.ncols, col0, Mt.y, Mt.N, s0 * 16u, lane, A.counters);
     }
     NF4_GSTAMP(5);
     }
     NF4_GSTAMP(9);
+}
+
+// ---------------------------------------------------------------------------
+// Balanced decode kernel (NF4DQ_GEMM_SK; M * K * 2 <= 64 KiB, K % 256 == 0).
+// The kernels above hand out whole 16-column strips (or groups of them) per
+// workgroup, and strips rarely divide over the CUs: 14336 columns = 896 strips
+// in groups of 4 keep 224 of 256 CUs busy (12.5 % idle), and the time until a
+// CU's first weight arrives is paid per workgroup.  Here the unit of work is one
+// (strip, 256-deep chunk) pair -- 2 KiB of packed weight, one 128-byte line of
+// each of the strip's 16 rows -- numbered strip-major over every weight of the
+// launch, and each wave of a one-workgroup-per-CU grid takes an equal
+// contiguous range of units (the "stream-K" decomposition, Osama et al.,
+// PPoPP 2023): every CU streams the same number of bytes, and a wave issues
+// its units' loads into a D-deep register ring before it builds the tables.
+//  * A wave's range is at most one strip long (host), so it holds at most two
+//    partial tiles: the end of one strip and the start of the next.
+//  * Ranges are contiguous in K within a strip, so a strip's partials are
+//    summed in range order (= K order): inside the workgroup through LDS (the x
+//    rows' region, free once every wave is done), and a strip shared with the
+//    neighbouring workgroup(s) through the split-K slab -- NOT-encoded relaxed
+//    atomics, one ticket per strip, the last arriver sums the slots in
+//    workgroup order (splitk_reduce): one launch, bitwise reproducible.
+//  * Dequant + MFMA per unit: the streaming kernels' pair-table body (sslot_mma),
+//    x[M][K] staged once per workgroup in LDS.
+struct SkArgs {
+    StreamMat mat[kGroupMax];
+    uint32_t nmat;
+    const void* x;
+    uint64_t* slab;      // [slot][M][ncols / 2] NOT-encoded partial pairs (strips shared by workgroups)
+    uint32_t* counters;  // one ticket per strip, 0 between calls
+    uint32_t M, K;
+    FastDiv C;           // 256-deep chunks per strip (K / 256)
+    FastDiv ppr;         // 16-byte x pieces per row (K / 8)
+    uint32_t U;          // units: strips x C
+    uint32_t GW;         // waves in the grid
+    uint32_t ncols;      // sum of N (slab row length)
+    uint32_t bpr, groups;
+    uint32_t xstride;    // LDS bytes per staged x row (16-B padded: rows 4 banks apart)
+    uint32_t zero_off;   // 128 zero bytes: the A operand of rows >= M
+};
+
+// First unit of grid wave g (g = GW: one past the last)
+__device__ __forceinline__ uint32_t sk_u0(const SkArgs& A, uint32_t g) {
+    return (uint32_t)(((uint64_t)g * A.U) / A.GW);
+}
+// The grid wave whose range holds unit u (the largest g with sk_u0(g) <= u)
+__device__ __forceinline__ uint32_t sk_wave_of(const SkArgs& A, uint32_t u) {
+    return (uint32_t)((((uint64_t)u + 1u) * A.GW - 1u) / A.U);
+}
+// The weight of a launch-wide strip (straight-line selects, uniform)
+__device__ __forceinline__ uint32_t sk_mat_of(const SkArgs& A, uint32_t strip) {
+    uint32_t mi = 0;
+#pragma unroll
+    for (int i = 1; i < kGroupMax; ++i) mi = (uint32_t)i < A.nmat && strip >= A.mat[i].strip_begin ? (uint32_t)i : mi;
+    return mi;
+}
+
+template <int DT, int W, int LM>
+__global__ __launch_bounds__(64 * W) void nf4_gemm_sk_kernel(const SkArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];  // x rows + zero block; later the partial tiles
+    __shared__ __attribute__((aligned(16))) f32x2 ptab[256 * 32];
+    __shared__ float qtab[256];
+    __shared__ uint32_t wrange[W][2];  // each wave's [first unit, units)
+    constexpr int D = LM < 4 ? LM : 4;  // ring depth: 4 x 2 KiB per wave, 16 waves = 128 KiB in flight per CU
+    constexpr int XP = 4096 / (64 * W);  // 16-byte x pieces per thread: 64 KiB of x at most
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t nl = lane & 15u, kh = lane >> 4;
+    const uint32_t gw0 = blockIdx.x * (uint32_t)W;
+    const uint32_t u0 = sk_u0(A, gw0 + wave), n = sk_u0(A, gw0 + wave + 1u) - u0;  // n <= LM, <= C (host)
+    const uint32_t Kh = A.K >> 1;
+
+    // 1. x rows (contiguous [M][K]: piece p at byte 16 p), issued first so that the
+    //    staging below waits for them alone
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
+    const uint32_t pieces = A.M * A.ppr.d;
+    u32x4 xv[XP];
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+        const uint32_t p = tid + (uint32_t)i * 64u * W;
+        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, p < pieces ? p * 16u : kOob, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 2. the ring: unit j of the wave = strip s, chunk c; lane (nl, kh) loads the 32
+    //    bytes of row nl at chunk c, quarter kh = one 64-block (one scale)
+    auto issue = [&](int j, SSlot& sl) {
+        const bool valid = (uint32_t)j < n;  // uniform; past the range: no traffic
+        const uint32_t u = valid ? u0 + (uint32_t)j : 0u;
+        const uint32_t s = fdiv(u, A.C), c = u - s * A.C.d;
+        const StreamMat& Mt = A.mat[sk_mat_of(A, s)];
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * Kh, kRsrcFlags);
+        const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a1, 0, Mt.nb_bytes, kRsrcFlags);
+        const __amdgpu_buffer_rsrc_t ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a2, 0, Mt.n2_bytes, kRsrcFlags);
+        const uint32_t row = (s - Mt.strip_begin) * 16u + nl;
+        const uint32_t oob = valid ? 0u : kOob;
+        const uint32_t woff = (row * Kh + c * 128u + kh * 32u) | oob;
+        sl.w0 = NF4_ABL_WLOAD(rw, woff);
+        sl.w1 = NF4_ABL_WLOAD(rw, woff + 16u);
+        // block 4c + kh of the row, nested group c (the reference's repeat wraps, :173-186)
+        sl.qa = __builtin_amdgcn_raw_buffer_load_b8(ra1, fmodu(row * A.bpr + 4u * c + kh, Mt.nb) | oob, 0, 0);
+        sl.qb = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(ra2, (fmodu(row * A.groups + c, Mt.n2) * 4u) | oob, 0, 0));
+    };
+    SSlot ring[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        issue(j, ring[j]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // 3. tables (no global data: they fill while the loads fly), the x rows, one barrier
+    if (tid < 256u) qtab[tid] = (float)tid / 127.0f;  // IEEE division (:45)
+    if (tid < 8u) *reinterpret_cast<u32x4*>(smem + A.zero_off + 16u * tid) = u32x4{0u, 0u, 0u, 0u};
+    if (lane == 0) {
+        wrange[wave][0] = u0;
+        wrange[wave][1] = n;
+    }
+    for (uint32_t u = tid; u < 16u * 32u; u += 64u * W) {
+        const float clo = nf4_code(u >> 5);
+#pragma unroll
+        for (int hi = 0; hi < 16; ++hi) ptab[(16u * hi + (u >> 5)) * 32u + (u & 31u)] = f32x2{nf4_code(hi), clo};
+    }
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+        const uint32_t p = tid + (uint32_t)i * 64u * W;
+        if (p < pieces) {
+            const uint32_t r = fdiv(p, A.ppr);
+            *reinterpret_cast<u32x4*>(smem + r * A.xstride + (p - r * A.ppr.d) * 16u) = xv[i];
+        }
+    }
+    __syncthreads();
+
+    // 4. the wave's units in order; the partial of the first strip is set aside
+    //    when the range crosses into the next (c wraps to 0)
+    const bool live = nl < A.M;
+    const uint32_t slot8 = (lane & 31u) * 8u;
+    f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, accb[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 part0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    bool split = false;
+#pragma unroll
+    for (int j = 0; j < LM; ++j) {
+        if ((uint32_t)j < n) {  // uniform
+            const uint32_t u = u0 + (uint32_t)j;
+            const uint32_t c = u - fdiv(u, A.C) * A.C.d;
+            if (j > 0 && c == 0u) {  // uniform: the range enters its second strip
+                part0 = acc[0] + accb[0];
+                acc[0] = accb[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                split = true;
+            }
+            const uint32_t xa[1] = {live ? nl * A.xstride + c * 512u + kh * 128u : A.zero_off};
+            sslot_mma<DT, 1>(ring[j % D], ring[j % D].qa, ring[j % D].qb, ptab, qtab, smem, slot8, xa, acc, accb);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (j + D < LM) issue(j + D, ring[j % D]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const f32x4 fin = acc[0] + accb[0];
+
+    // 5. partial tiles into the x region (every wave is done reading x), then per
+    //    strip of the workgroup's range one wave sums them in wave (= K) order
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smem);  // [W][2][64]
+    red[(wave * 2u) * 64u + lane] = split ? part0 : fin;
+    if (split) red[(wave * 2u + 1u) * 64u + lane] = fin;
+    __syncthreads();
+    const uint32_t U0 = sk_u0(A, gw0), U1 = sk_u0(A, gw0 + W);  // the workgroup's units (>= 1: host)
+    const uint32_t sA = fdiv(U0, A.C), sB = fdiv(U1 - 1u, A.C);
+    for (uint32_t s = sA + wave; s <= sB; s += W) {  // uniform
+        const uint32_t cs = s * A.C.d, ce = cs + A.C.d;
+        f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+        bool have = false;
+        for (uint32_t w = 0; w < (uint32_t)W; ++w) {
+            const uint32_t a0 = wrange[w][0], a1 = a0 + wrange[w][1];
+            if (a1 <= a0 || a1 <= cs || a0 >= ce) continue;  // uniform: no units in strip s
+            const f32x4 v = red[(w * 2u + (a0 >= cs ? 0u : 1u)) * 64u + lane];
+            sum = have ? sum + v : v;
+            have = true;
+        }
+        const StreamMat& Mt = A.mat[sk_mat_of(A, s)];
+        const uint32_t ycol = (s - Mt.strip_begin) * 16u;
+        if (cs >= U0 && ce <= U1) {  // the whole strip is this workgroup's: sum[r] = Y[4 kh + r][col nl]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t m = 4u * kh + (uint32_t)r;
+                if (m < A.M) store_y<DT>(Mt.y, m * Mt.N + ycol + nl, sum[r]);
+            }
+            continue;
+        }
+        // shared with the neighbouring workgroup(s): slot = this workgroup's place among them
+        const uint32_t g_first = sk_wave_of(A, cs) / (uint32_t)W, g_last = sk_wave_of(A, ce - 1u) / (uint32_t)W;
+        const uint32_t slot = blockIdx.x - g_first, nsl = g_last - g_first + 1u;
+        const uint32_t scol = s * 16u + nl;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t m = 4u * kh + (uint32_t)r;
+            slab_put_lane(A.slab, slab_entry(slot, A.M, m, A.ncols, scol), sum[r], nl, m < A.M);
+        }
+        uint32_t last = 0;
+        if (lane == 0) last = splitk_ticket(&A.counters[s], nsl);
+        last = __builtin_amdgcn_readfirstlane(last);
+        if (last) splitk_reduce<DT, 16u>(A.slab, nsl, A.M, A.ncols, s * 16u, Mt.y, Mt.N, ycol, lane, A.counters);
+    }
 }
 
 // ---- decomposition choice --------------------------------------------------
@@ -1968,6 +2197,11 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
         const int64_t chunks = K / kChunkK, per = (int64_t)c.waves * c.strips;
         return c.ksplit == (chunks + per - 1) / per && c.ksplit <= 1024;
     }
+    if (c.kernel == NF4DQ_GEMM_SK) {
+        // static rules only: whether the launch's column total spreads over the CUs is
+        // checked at launch (sk_plan; a grouped launch counts every weight's columns)
+        return K % kSChunkK == 0 && M * K * 2 <= 65536 && c.waves == 16 && c.ksplit == 1;
+    }
     if (c.kernel == NF4DQ_GEMM_XS) {
         if (c.waves != 4 && c.waves != 8) return false;
         if (c.depth != 2 && c.depth != 4 && c.depth != 8) return false;
@@ -1986,14 +2220,21 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 inline int hip_rc2(hipError_t e) { return e == hipSuccess ? NF4DQ_OK : NF4DQ_ERR_HIP_BASE + (int)e; }
 
-// Workspace: [64 KiB of uint32 ticket counters][ksplit * M * N / 2 64-bit slab entries].
-// The counter region has a fixed size so that no call's partials ever overlay
-// another call's counters (those must stay 0 between calls): N <= 2^18.
+// Workspace: [64 KiB of uint32 ticket counters][256 B: the error word + spare]
+// [ksplit * M * N / 2 64-bit slab entries].  The header has a fixed size so that no
+// call's partials ever overlay another call's counters (those must stay 0 between
+// calls): N <= 2^18.  The error word (kErrWord, sticky) is set by a reducer whose
+// poll gave up (nf4_gemm_check_workspace reads it).
 constexpr size_t kCounterBytes = 64 * 1024;
-static size_t counters_bytes(int64_t) { return kCounterBytes; }
+constexpr size_t kHeaderBytes = kCounterBytes + 256;
+static_assert(kErrWord * 4u == kCounterBytes, "the error word follows the counters");
+static size_t counters_bytes(int64_t) { return kHeaderBytes; }
+
+static size_t sk_workspace(int64_t M, int64_t K, int64_t ncols, int waves);
 
 static size_t workspace_for(int64_t M, int64_t N, int64_t K, const nf4_gemm_cfg& c) {
     if (M <= 0 || N <= 0 || K <= 0 || N % 64 || K % kChunkK) return 0;
+    if (c.kernel == NF4DQ_GEMM_SK) return sk_workspace(M, K, N, c.waves);
     return c.ksplit > 1 ? counters_bytes(N) + (size_t)c.ksplit * (size_t)M * (size_t)N * 4u : 0;  // 8-B entry per 2 columns
 }
 
@@ -2030,7 +2271,7 @@ static int launch_stream(const HostMat* mats, int count, const void* x, int64_t 
     S.nmat = (uint32_t)count;
     S.x = x;
     S.counters = reinterpret_cast<uint32_t*>(workspace);
-    S.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    S.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kHeaderBytes) : nullptr;
     S.M = (uint32_t)M;
     S.K = (uint32_t)K;
     S.T = (uint32_t)cfg.strips;
@@ -2123,7 +2364,7 @@ static int launch_persist(const HostMat* mats, int count, const void* x, int64_t
     S.nmat = (uint32_t)count;
     S.x = x;
     S.counters = reinterpret_cast<uint32_t*>(workspace);
-    S.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    S.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kHeaderBytes) : nullptr;
     S.M = (uint32_t)M;
     S.K = (uint32_t)K;
     S.T = (uint32_t)cfg.strips;
@@ -2228,7 +2469,7 @@ static int launch_xs(const HostMat* mats, int count, const void* x, int64_t M, i
     A.nmat = (uint32_t)count;
     A.x = x;
     A.counters = reinterpret_cast<uint32_t*>(workspace);
-    A.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    A.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kHeaderBytes) : nullptr;
     A.M = (uint32_t)M;
     A.K = (uint32_t)K;
     A.ksplit = ks;
@@ -2323,7 +2564,7 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
     A.nmat = (uint32_t)count;
     A.x = x;
     A.counters = reinterpret_cast<uint32_t*>(workspace);
-    A.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    A.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kHeaderBytes) : nullptr;
     A.M = (uint32_t)M;
     A.K = (uint32_t)K;
     A.ksplit = ks;
@@ -2409,6 +2650,122 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
     return hip_rc2(hipGetLastError());
 }
 
+// Balanced kernel plan (nf4_gemm_sk_kernel): one workgroup of 16 waves per CU,
+// units = strips x (K / 256) split evenly over the waves.  Runs when x fits its
+// LDS (M K 2 <= 64 KiB), every workgroup gets a unit, and a wave's range is at
+// most one strip and 16 units long.  `slots`: most workgroups sharing one strip
+// (the split-K slab holds that many slices; 1 = no strip is shared).
+struct SkPlan {
+    uint32_t G, W, GW, C, LM, slots, xstride, zero_off, lds;
+    uint64_t U;
+};
+
+static bool sk_plan(int64_t M, int64_t K, int64_t ncols, int waves, SkPlan& p) {
+    if (M < 1 || M > 16 || K <= 0 || K % kSChunkK || M * K * 2 > 65536 || ncols <= 0 || ncols % 16) return false;
+    if (waves != 16) return false;
+    p.W = (uint32_t)waves;
+    p.G = (uint32_t)device_cus();
+    p.GW = p.G * p.W;
+    p.C = (uint32_t)(K / kSChunkK);
+    const uint64_t strips = (uint64_t)ncols / 16u;
+    p.U = strips * p.C;
+    if (p.U >= (uint64_t(1) << 31) || p.U < p.G) return false;  // every workgroup gets >= 1 unit
+    const uint64_t L = (p.U + p.GW - 1) / p.GW;                 // longest wave range
+    if (L > p.C) return false;                                  // <= one strip: two partial tiles at most
+    uint32_t lm = 1;
+    while (lm < L) lm *= 2;
+    if (lm > 16) return false;
+    p.LM = lm;
+    const uint64_t GW = p.GW, U = p.U;
+    auto wg_of = [&](uint64_t u) { return ((u + 1) * GW - 1) / U / p.W; };
+    uint64_t slots = 1;
+    for (uint64_t s = 0; s < strips; ++s) {
+        const uint64_t a = wg_of(s * p.C), b = wg_of(s * p.C + p.C - 1);
+        slots = b - a + 1 > slots ? b - a + 1 : slots;
+    }
+    p.slots = (uint32_t)slots;
+    p.xstride = (uint32_t)K * 2u + 16u;
+    p.zero_off = (uint32_t)M * p.xstride;
+    const uint32_t xb = p.zero_off + 128u, rb = p.W * 2u * 64u * 16u;
+    p.lds = xb > rb ? xb : rb;
+    return p.lds + kStreamStatic + 2u * 4u * p.W <= kLdsPerCu;
+}
+
+static size_t sk_workspace(int64_t M, int64_t K, int64_t ncols, int waves) {
+    SkPlan p{};
+    if (!sk_plan(M, K, ncols, waves, p) || p.slots < 2) return 0;
+    return kHeaderBytes + (size_t)p.slots * (size_t)M * (size_t)ncols * 4u;  // 8-B entry per 2 columns
+}
+
+static int launch_sk(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
+                     const nf4_gemm_cfg& cfg, void* workspace, size_t workspace_bytes, hipStream_t st) {
+    int64_t ncols = 0;
+    for (int i = 0; i < count; ++i) ncols += mats[i].N;
+    SkPlan p{};
+    if (!sk_plan(M, K, ncols, cfg.waves, p)) return NF4DQ_ERR_ARG;
+    if (p.slots > 1 && (!workspace || workspace_bytes < sk_workspace(M, K, ncols, cfg.waves) || !aligned16(workspace)))
+        return NF4DQ_ERR_ARG;
+    SkArgs A{};
+    A.nmat = (uint32_t)count;
+    A.x = x;
+    A.counters = reinterpret_cast<uint32_t*>(workspace);
+    A.slab = p.slots > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kHeaderBytes) : nullptr;
+    A.M = (uint32_t)M;
+    A.K = (uint32_t)K;
+    A.C = make_fastdiv(p.C);
+    A.ppr = make_fastdiv((uint32_t)(K / 8));
+    A.U = (uint32_t)p.U;
+    A.GW = p.GW;
+    A.ncols = (uint32_t)ncols;
+    A.bpr = (uint32_t)(K / 64);
+    A.groups = (A.bpr + 3) / 4;
+    A.xstride = p.xstride;
+    A.zero_off = p.zero_off;
+    uint32_t strips = 0;
+    for (int i = 0; i < count; ++i) {
+        const HostMat& h = mats[i];
+        StreamMat& m = A.mat[i];
+        m.packed = h.packed;
+        m.a1 = h.a1;
+        m.a2 = h.a2;
+        m.y = h.y;
+        m.N = (uint32_t)h.N;
+        m.sg_begin = 0;
+        m.strip_begin = strips;
+        const int64_t nbc = h.nb > (int64_t(1) << 31) ? (int64_t(1) << 31) : h.nb;
+        const int64_t n2c = h.n2 > (int64_t(1) << 29) ? (int64_t(1) << 29) : h.n2;
+        m.nb = make_fastdiv((uint32_t)nbc);
+        m.n2 = make_fastdiv((uint32_t)n2c);
+        m.nb_bytes = (uint32_t)nbc;
+        m.n2_bytes = (uint32_t)(n2c * 4);
+        strips += (uint32_t)(h.N / 16);
+    }
+    const dim3 grid(p.G), block(64 * p.W);
+#define NF4_SK1(DT_, LM_)                                                                                  \
+    do {                                                                                                   \
+        static bool attr_ = false; /* static + dynamic LDS above 64 KiB needs the opt-in */                \
+        if (!attr_) {                                                                                      \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_sk_kernel<DT_, 16, LM_>),    \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsCap);     \
+            attr_ = true;                                                                                  \
+        }                                                                                                  \
+        hipLaunchKernelGGL((nf4_gemm_sk_kernel<DT_, 16, LM_>), grid, block, p.lds, st, A);                 \
+    } while (0)
+#define NF4_SKL(DT_)                          \
+    do {                                      \
+        if (p.LM == 1) NF4_SK1(DT_, 1);       \
+        else if (p.LM == 2) NF4_SK1(DT_, 2);  \
+        else if (p.LM == 4) NF4_SK1(DT_, 4);  \
+        else if (p.LM == 8) NF4_SK1(DT_, 8);  \
+        else NF4_SK1(DT_, 16);                \
+    } while (0)
+    if (dtype == NF4DQ_BF16) NF4_SKL(NF4DQ_BF16);
+    else NF4_SKL(NF4DQ_F16);
+#undef NF4_SKL
+#undef NF4_SK1
+    return hip_rc2(hipGetLastError());
+}
+
 static int launch_k128(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
                        const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st) {
     const uint32_t ks = (uint32_t)cfg.ksplit;
@@ -2417,7 +2774,7 @@ static int launch_k128(const HostMat* mats, int count, const void* x, int64_t M,
     A.nmat = (uint32_t)count;
     A.x = x;
     A.counters = reinterpret_cast<uint32_t*>(workspace);
-    A.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kCounterBytes) : nullptr;
+    A.slab = ks > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kHeaderBytes) : nullptr;
     A.M = (uint32_t)M;
     A.K = (uint32_t)K;
     A.ksplit = ks;
@@ -2526,6 +2883,7 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
         return launch_stream(&h, 1, x, M, K, dtype, cfg, workspace, st);
     }
     const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
+    if (cfg.kernel == NF4DQ_GEMM_SK) return launch_sk(&h, 1, x, M, K, dtype, cfg, workspace, workspace_bytes, st);
     if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(&h, 1, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_XR) return launch_xr(&h, 1, x, M, K, dtype, cfg, workspace, st);
     return launch_k128(&h, 1, x, M, K, dtype, cfg, workspace, st);
@@ -2559,14 +2917,15 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
         // an empty weight cannot own strip groups (the 128-deep kernel numbers
         // column groups per weight: an empty one simply owns none)
         if (mats[i].N == 0 && cfg.kernel != NF4DQ_GEMM_K128 && cfg.kernel != NF4DQ_GEMM_XS &&
-            cfg.kernel != NF4DQ_GEMM_XR)
+            cfg.kernel != NF4DQ_GEMM_XR && cfg.kernel != NF4DQ_GEMM_SK)
             return NF4DQ_ERR_SHAPE;
         if (mats[i].N == 0) continue;
         if (!valid_gemm_cfg(cfg, M, mats[i].N, K)) return NF4DQ_ERR_ARG;
         if (mats[i].packed_len >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
     }
     if (M * K * 2 >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
-    const size_t need = cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
+    const size_t need = cfg.kernel == NF4DQ_GEMM_SK ? sk_workspace(M, K, ntot, cfg.waves)
+                        : cfg.ksplit > 1 ? kHeaderBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
     if (need >= (size_t(1) << 32)) return NF4DQ_ERR_TOO_LARGE;  // one buffer descriptor over the slab
     if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
     HostMat h[NF4DQ_GEMM_GROUP_MAX];
@@ -2574,6 +2933,7 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
         h[i] = HostMat{mats[i].packed, mats[i].packed_len, mats[i].absmax_q, mats[i].nb, mats[i].absmax2,
                        mats[i].n2, mats[i].y, mats[i].N};
     if (cfg.kernel == NF4DQ_GEMM_K128) return launch_k128(h, count, x, M, K, dtype, cfg, workspace, st);
+    if (cfg.kernel == NF4DQ_GEMM_SK) return launch_sk(h, count, x, M, K, dtype, cfg, workspace, workspace_bytes, st);
     if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_XR) return launch_xr(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
@@ -2603,7 +2963,8 @@ static size_t grouped_workspace(int64_t M, int64_t K, const nf4_gemm_mat* mats, 
     if (ntot <= 0) return 0;
     nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, ntot, K);
     if (cfg.kernel == 0) cfg.kernel = default_gemm_cfg(M, ntot, K).kernel;
-    size_t w = cfg.ksplit > 1 ? kCounterBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
+    size_t w = cfg.kernel == NF4DQ_GEMM_SK ? sk_workspace(M, K, ntot, cfg.waves)
+               : cfg.ksplit > 1 ? kHeaderBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
     if (cfgp || cfg.kernel != NF4DQ_GEMM_PERSIST) return w;
     // the library's persistent choice may fall back to per-weight launches
     // (gemm_grouped_impl): the largest of their needs as well
@@ -2649,6 +3010,22 @@ int nf4_gemm_ref_grouped(const void* x, int64_t M, int64_t K, const nf4_gemm_mat
                          void* hip_stream) {
     return gemm_grouped_impl(x, M, K, mats, count, out_dtype, workspace, workspace_bytes, cfg,
                              reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+int nf4_gemm_check_workspace(void* workspace, size_t workspace_bytes, void* hip_stream) {
+    if (!workspace || workspace_bytes == 0) return NF4DQ_OK;  // no split-K ran on it
+    if (workspace_bytes < kHeaderBytes) return NF4DQ_ERR_ARG;  // never a split-K workspace
+    const hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+    uint32_t err = 0;
+    hipError_t e = hipMemcpyAsync(&err, reinterpret_cast<char*>(workspace) + kCounterBytes, sizeof(err),
+                                  hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_rc2(e);
+    if (!err) return NF4DQ_OK;
+    // every kernel of the stream has finished: no late store can land after this
+    e = hipMemsetAsync(workspace, 0, workspace_bytes, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e != hipSuccess ? hip_rc2(e) : NF4DQ_ERR_SPLITK_TIMEOUT;
 }
 
 int nf4_gemm_ref_cfg(const void* x, int64_t M, const uint8_t* packed, int64_t packed_len, const uint8_t* absmax_q,

@@ -1,4 +1,4 @@
-"""Multi-GPU: independent NF4 weights sharded one-per-GPU, quant_state broadcast over RCCL.
+"""Multi-GPU: independent NF4 weights sharded one-per-GPU, quant_state scattered over RCCL.
 
 Scope (BASELINE.json config 5): dequantization has no exchange step
 -- every weight matrix (and every row) is independent -- so ranks split the
@@ -7,8 +7,11 @@ the distribution of the quantization statistics (``absmax`` u8 + nested
 ``state2.absmax`` fp32 + shape metadata) from the rank that loaded them, done
 once at setup: ``scatter_quant_stats`` sends each rank only its own matrices'
 statistics (per-destination point-to-point messages posted together, one xGMI
-link each), ``broadcast_quant_stats`` gives every rank everything (coalesced:
-one u8 buffer, one fp32 buffer rather than one message per matrix).  The packed 4-bit weights are resident on (or
+link each) -- what bench.py uses, by design instead of BASELINE's "RCCL broadcast
+of quant_state": at C5 / N = 8 a rank receives 1 MiB + 16 KiB rather than all
+8.5 MB; ``broadcast_quant_stats`` gives every rank everything (coalesced:
+one u8 buffer, one fp32 buffer rather than one message per matrix).  ``src`` is a
+rank of ``group`` in both (converted to the global rank the collectives take).  The packed 4-bit weights are resident on (or
 loaded by) the rank that owns them and never cross the link.
 
 One process per GPU, ``torch.distributed`` backend ``nccl`` (= RCCL on ROCm);
@@ -53,6 +56,7 @@ def broadcast_quant_stats(stats: Optional[Sequence[QuantStats]], device: torch.d
     nested absmax.  Returns the full list on every rank, on ``device``.
     """
     rank = dist.get_rank(group)
+    gsrc = _global(src, group)  # collectives take the source's global rank
     if rank == src:
         if stats is None:
             raise ValueError("source rank must provide stats")
@@ -60,19 +64,24 @@ def broadcast_quant_stats(stats: Optional[Sequence[QuantStats]], device: torch.d
         count = torch.tensor([meta.shape[0]], dtype=torch.int64, device=device)
     else:
         count = torch.zeros(1, dtype=torch.int64, device=device)
-    dist.broadcast(count, src, group=group)
+    dist.broadcast(count, gsrc, group=group)
     k = int(count.item())
     meta_d = meta.to(device) if rank == src else torch.zeros((k, 5), dtype=torch.int64, device=device)
-    dist.broadcast(meta_d, src, group=group)
+    dist.broadcast(meta_d, gsrc, group=group)
     meta_h = meta_d.cpu()
     if rank != src:
         a1 = torch.empty(int(meta_h[:, 2].sum()) if k else 0, dtype=torch.uint8, device=device)
         a2 = torch.empty(int(meta_h[:, 3].sum()) if k else 0, dtype=torch.float32, device=device)
     if a1.numel():
-        dist.broadcast(a1, src, group=group)
+        dist.broadcast(a1, gsrc, group=group)
     if a2.numel():
-        dist.broadcast(a2, src, group=group)
+        dist.broadcast(a2, gsrc, group=group)
     return _unpack(meta_h, a1, a2)
+
+
+def _global(r: int, group) -> int:
+    """Global rank of group rank ``r`` (``src`` arguments here are group ranks)."""
+    return r if group is None else dist.get_global_rank(group, r)
 
 
 def _pack(stats: Sequence[QuantStats], device: torch.device):
@@ -119,7 +128,7 @@ def scatter_quant_stats(per_rank: Optional[Sequence[Sequence[QuantStats]]], devi
     else:
         sizes = None
     mine_sz = torch.zeros(3, dtype=torch.int64, device=device)
-    dist.scatter(mine_sz, sizes, src=src, group=group)
+    dist.scatter(mine_sz, sizes, src=_global(src, group), group=group)
     k, nb_tot, n2_tot = (int(v) for v in mine_sz.cpu())
     if rank == src:
         reqs = []
@@ -127,7 +136,7 @@ def scatter_quant_stats(per_rank: Optional[Sequence[Sequence[QuantStats]]], devi
             if r == src:
                 continue
             meta, a1, a2 = packed[r]
-            peer = r if group is None else dist.get_global_rank(group, r)
+            peer = _global(r, group)
             for t in (meta.to(device), a1, a2):
                 if t.numel():
                     reqs.append(dist.isend(t.contiguous(), peer, group=group))
@@ -138,7 +147,7 @@ def scatter_quant_stats(per_rank: Optional[Sequence[Sequence[QuantStats]]], devi
     meta_d = torch.zeros((k, 5), dtype=torch.int64, device=device)
     a1 = torch.empty(nb_tot, dtype=torch.uint8, device=device)
     a2 = torch.empty(n2_tot, dtype=torch.float32, device=device)
-    peer = src if group is None else dist.get_global_rank(group, src)
+    peer = _global(src, group)
     reqs = [dist.irecv(t, peer, group=group) for t in (meta_d, a1, a2) if t.numel()]
     for q in reqs:
         q.wait()

@@ -37,6 +37,7 @@ def test_header_constants_match_binding():
     assert int(consts["NF4DQ_ERR_ARG"]) == _lib.ERR_ARG
     assert int(consts["NF4DQ_ERR_SHAPE"]) == _lib.ERR_SHAPE
     assert int(consts["NF4DQ_BATCH_MAX"]) == _lib.BATCH_MAX
+    assert int(consts["NF4DQ_ERR_SPLITK_TIMEOUT"]) == _lib.ERR_SPLITK_TIMEOUT
 
 
 def test_struct_layouts():
@@ -49,6 +50,15 @@ def test_version_and_strerror():
     assert b"gfx950" in L.nf4_version()
     assert L.nf4_strerror(0) == b"ok"
     assert b"shape" in L.nf4_strerror(2)
+    assert b"split-K" in L.nf4_strerror(_lib.ERR_SPLITK_TIMEOUT)
+
+
+def test_check_workspace_host_validation():
+    """nf4_gemm_check_workspace: nothing to report without a workspace; a buffer too
+    small to hold the header was never a split-K workspace (host checks, no device call)."""
+    L = _lib.lib()
+    assert L.nf4_gemm_check_workspace(None, 0, None) == _lib.OK
+    assert L.nf4_gemm_check_workspace(FAKE, 1024, None) == _lib.ERR_ARG
 
 
 FAKE = 0x1000  # never dereferenced: every call below fails validation first
@@ -110,7 +120,7 @@ def test_cfg_validation():
     L = _lib.lib()
     cfg = _lib.LaunchCfg(3, 0, 0, 0)
     assert L.nf4_dequant_ref_cfg(FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, ctypes.byref(cfg), None) == _lib.ERR_ARG
-    # only tile_dwords 4, nontemporal 1, a grid cap >= 0 and the absmax prefetch field remain
+    # only tile_dwords 4, nontemporal 1 and a grid cap >= 0 remain; flags is reserved and must be 0
     for bad in ((8, 0, 1, 0), (2, 0, 1, 0), (4, 0, 0, 0), (4, -1, 1, 0), (4, 0, 1, 1), (4, 0, 1, 0x8),
                 (4, 0, 1, 0x100), (4, 0, 1, 0x2000), (4, 0, 1, 0x10000)):
         cfg = _lib.LaunchCfg(*bad)

@@ -121,3 +121,46 @@ def test_scatter_sends_each_rank_only_its_own(world):
     for r, ok, k, nbytes, nempty in res:
         assert ok and k == len(owned[r]) and nempty == 0
         assert nbytes == sum(int(ref[i].absmax.numel()) for i in owned[r])
+
+
+def _subgroup_worker(rank, world, port, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sub = dist.new_group([1, 2])  # every rank creates it; group rank 0 = global rank 1
+        res = (rank, None, None)
+        if rank in (1, 2):
+            ref = _stats(5)
+            owned = assign_round_robin(len(ref), 2)
+            grank = dist.get_rank(sub)
+            per_rank = [[ref[i] for i in owned[r]] for r in range(2)] if grank == 0 else None
+            got = scatter_quant_stats(per_rank, torch.device("cpu"), src=0, group=sub)
+            want = [ref[i] for i in owned[grank]]
+            ok_s = len(got) == len(want) and all(
+                torch.equal(a.absmax, b.absmax) and torch.equal(a.absmax2, b.absmax2) for a, b in zip(got, want))
+            allb = broadcast_quant_stats(ref if grank == 0 else None, torch.device("cpu"), src=0, group=sub)
+            ok_b = len(allb) == len(ref) and all(torch.equal(a.absmax, b.absmax) for a, b in zip(allb, ref))
+            res = (rank, ok_s, ok_b)
+        result_q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_scatter_and_broadcast_in_a_subgroup():
+    """``src`` is a group rank: in a subgroup whose rank 0 is global rank 1, the scatter
+    and the broadcast still start from that rank (dist.scatter takes the
+    global rank)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=90) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[0] == (0, None, None)
+    assert res[1] == (1, True, True) and res[2] == (2, True, True)

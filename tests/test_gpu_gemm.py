@@ -214,15 +214,17 @@ def test_every_decomposition_agrees_with_oracle(coracle, gpu, dt, M, N, K):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
-@pytest.mark.parametrize("M,K,kpw,spw", [(32, 4096, 2, 3), (32, 4096, 2, 9), (17, 4096, 2, 3), (32, 2048, 1, 3),
-                                         (24, 4096, 4, 3)])
+@pytest.mark.parametrize("M,K,kpw,spw", [(32, 4096, 2, 3), (32, 4096, 2, 9), (32, 4096, 2, 17), (17, 4096, 2, 3),
+                                         (32, 2048, 1, 3), (24, 4096, 4, 3)])
 def test_xr_multi_strip_workgroups(coracle, gpu, dt, M, K, kpw, spw):
     """The register-resident kernel with several 16-column strips per workgroup, at
     any CU count: N is sized from the device's CUs so that every workgroup walks >= spw
     strips (its ring refills, partial-tile reduction groups and cached weight
-    descriptors all cross strip boundaries).  At two K slices, spw = 3 takes the
-    unrolled-group form (exchanges inside the strip loop, <= 8 strips per workgroup)
-    and spw = 9 the looped form (exchanges after it)."""
+    descriptors all cross strip boundaries).  At two K slices (kpw = 2) the exchange
+    form follows the strips per workgroup (launch_xr): spw = 3 takes the unrolled
+    groups with GU = 4 (<= 8 strips), spw = 9 GU = 8 (<= 16 strips), both exchanging
+    inside the strip loop, and spw = 17 the looped form (exchanges after the loop);
+    kpw = 1 (four K slices) takes the ticket-and-poll hand-off."""
     from nf4_triton_dequantization_amd import _lib
 
     L = _lib.lib()
@@ -735,3 +737,77 @@ try:
             _check(y, xb, W, "bf16")
 except ImportError:  # hypothesis is part of the test environment; keep the module importable without it
     pass
+
+
+def _sk_call(L, _lib, x, mats, dt_code, K):
+    """One NF4DQ_GEMM_SK launch over `mats` [(packed, a1, a2, y)] through the grouped
+    ABI (one weight = a group of one); returns (rc, workspace)."""
+    import ctypes
+
+    M = x.shape[0]
+    cfg = _lib.GemmCfg(_lib.GEMM_SK, 16, 0, 1, 0)
+    arr = (_lib.GemmMat * len(mats))()
+    for i, (p, a1, a2, y) in enumerate(mats):
+        arr[i] = _lib.GemmMat(p.data_ptr(), p.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                              y.data_ptr(), y.shape[1])
+    wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, arr, len(mats), ctypes.byref(cfg))
+    ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=x.device)
+    st = torch.cuda.current_stream().cuda_stream
+    rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, arr, len(mats), dt_code, ws.data_ptr() if wsz else None, wsz,
+                                ctypes.byref(cfg), st)
+    chk = L.nf4_gemm_check_workspace(ws.data_ptr() if wsz else None, wsz, st)
+    torch.cuda.synchronize()
+    return rc, chk, ws, wsz
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,Ns,K", [(1, (14336,), 4096), (4, (4096,), 4096), (8, (1024,), 4096), (1, (4096,), 14336),
+                                    (3, (4160,), 1280), (16, (2048,), 2048), (1, (4096, 1024, 1024), 4096),
+                                    (2, (14336, 14336), 4096), (5, (64, 4096, 192), 2048)])
+def test_balanced_kernel(coracle, gpu, dt, M, Ns, K):
+    """NF4DQ_GEMM_SK: equal (strip, 256-deep chunk) ranges per wave, strips shared by
+    workgroups summed through the slab (the 1024-column weight: four workgroups per
+    strip; 4160 x 1280: ragged strip count, 5 chunks per strip; down projection: 56;
+    grouped launches with a 64-column weight inside a group).  Checked against the
+    float64 oracle of the reference's weights, the workspace back at zero with no
+    split-K error, and a second launch bitwise identical (fixed summation order)."""
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    code = _lib.BF16 if dt == "bf16" else _lib.F16
+    xt, xb = _x_bits(M, K, dt, seed=M * 11 + K)
+    x = xt.to(gpu)
+    mats, Ws = [], []
+    for i, N in enumerate(Ns):
+        packed, a1, a2 = O.make_inputs(N, K, seed=N + K + M + 31 * i, a2_kind="normal")
+        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16))
+        mats.append((torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu),
+                     torch.full((M, N), float("nan"), dtype=x.dtype, device=gpu)))
+    rc, chk, ws, wsz = _sk_call(L, _lib, x, mats, code, K)
+    assert rc == 0, _lib.strerror(rc)
+    assert chk == 0, _lib.strerror(chk)
+    if wsz:
+        assert int(ws.count_nonzero()) == 0, "tickets / slab entries not back at 0"
+    first = [m[3].clone() for m in mats]
+    for (_, _, _, y), W in zip(mats, Ws):
+        assert not bool(torch.isnan(y).any())
+        _check(y, xb, W, dt)
+    rc, chk, _, _ = _sk_call(L, _lib, x, mats, code, K)
+    assert rc == 0 and chk == 0
+    for y0, m in zip(first, mats):
+        assert torch.equal(y0.view(torch.int16), m[3].view(torch.int16)), "not bitwise reproducible"
+
+
+def test_balanced_kernel_rejects_what_it_cannot_spread(gpu):
+    """Fewer units than CUs, x beyond its LDS, or a K not a multiple of 256: ERR_ARG, no launch."""
+    import ctypes
+
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    F = 0x1000
+    c = _lib.GemmCfg(_lib.GEMM_SK, 16, 0, 1, 0)
+    for (M, N, K) in [(1, 64, 2048), (9, 4096, 4096), (1, 4096, 1152), (33, 4096, 4096)]:
+        rc = L.nf4_gemm_ref_cfg(F, M, F, N * K // 2, F, N * K // 64, F, 16, F, _lib.BF16, N, K, F, 1 << 30,
+                                ctypes.byref(c), None)
+        assert rc in (_lib.ERR_ARG, _lib.ERR_SHAPE), (M, N, K, rc)

@@ -179,9 +179,9 @@ def test_batched_matches_single_calls(coracle, gpu):
         assert_bits_equal(out_bits(o), w, "f16", f"batched into #{i}")
 
 
-# the launch knobs the library keeps (include/nf4_dequant.h): grid cap (persistent
-# waves walking several tiles; 1 and 3 workgroups per CU give odd and even tile
-# counts, so both loop exits run) and the absmax L2 prefetch distance
+# the one launch knob the library keeps (include/nf4_dequant.h): the grid cap
+# (persistent waves walking several tiles; 1 and 3 workgroups per CU give odd and
+# even tile counts, so both loop exits run); flags is reserved (0)
 @pytest.mark.parametrize("cfg", [(4, 0, 1, 0), (4, 1, 1, 0), (4, 2, 1, 0), (4, 3, 1, 0), (4, 8, 1, 0)])
 def test_launch_configs_identical(coracle, gpu, cfg):
     from nf4_triton_dequantization_amd import _lib

@@ -6,7 +6,8 @@ handed -- inputs, outputs, the GEMM workspace -- is carved out of a larger
 allocation with 64 KiB guard bands of a fixed byte pattern on both sides.  After
 each call: both bands of every buffer intact (no write outside a buffer), the
 inputs unchanged (no write into an input), the output equal to the oracle, and
-the split-K ticket counters and slab entries back at zero.  Shapes take ragged tails (partial
+the split-K ticket counters, error word and slab entries back at zero
+(nf4_gemm_check_workspace returns OK).  Shapes take ragged tails (partial
 tiles, partial 64-blocks, odd n, single rows, wrapping / truncated statistics,
 strips not filling a workgroup), where range handling matters.
 (The host path has its own ASan/UBSan run: tests/test_cpu_sanitizers.py.)
@@ -24,7 +25,8 @@ pytestmark = pytest.mark.gpu
 
 GUARD = 64 * 1024
 PAT = 0xA5
-COUNTER_BYTES = 64 * 1024  # split-K tickets at the head of the GEMM workspace (nf4_gemm.hip kCounterBytes)
+COUNTER_BYTES = 64 * 1024  # split-K tickets at the head of the GEMM workspace (nf4_gemm.hip kCounterBytes);
+# the error word and 252 spare bytes follow (kHeaderBytes = 64 KiB + 256), then the slab
 
 
 class Guarded:
@@ -166,6 +168,7 @@ def _gemm_cfgs(K):
         for depth in (2, 4):
             for kpw in (1, 2, 4):
                 yield _lib.GemmCfg(_lib.GEMM_XR, waves, depth, -(-chunks // (waves * kpw)), kpw)
+    yield _lib.GemmCfg(_lib.GEMM_SK, 16, 0, 1, 0)  # balanced kernel (ERR_ARG where it cannot spread)
 
 
 def _gemm_ref(W_bits, x_bits):
@@ -176,7 +179,8 @@ def _gemm_ref(W_bits, x_bits):
     return ref, tol
 
 
-@pytest.mark.parametrize("M,N,K", [(3, 192, 384), (17, 4160, 1280), (32, 2112, 4096), (1, 64, 2048)])
+@pytest.mark.parametrize("M,N,K", [(3, 192, 384), (17, 4160, 1280), (32, 2112, 4096), (1, 64, 2048),
+                                   (5, 4160, 1280), (2, 1024, 4096)])
 def test_gemm_every_decomposition(coracle, gpu, M, N, K):
     from nf4_triton_dequantization_amd import _lib
 
@@ -202,6 +206,8 @@ def test_gemm_every_decomposition(coracle, gpu, M, N, K):
         assert rc == 0, (what, _lib.strerror(rc))
         assert y.bands_intact(), f"write outside y, cfg {what}"
         assert ws.bands_intact(), f"write outside the workspace, cfg {what}"
+        # the split-K error word: no reducer gave up
+        assert L.nf4_gemm_check_workspace(ws.ptr() if wsz else None, wsz, _stream()) == 0, what
         if wsz:
             # tickets back at 0 and every split-K slab entry read and cleared (empty) again
             assert int(ws.body()[:min(COUNTER_BYTES, wsz)].count_nonzero()) == 0, f"tickets not reset, cfg {what}"
@@ -237,6 +243,7 @@ def test_gemm_grouped(coracle, gpu):
     torch.cuda.synchronize()
     assert rc == 0, _lib.strerror(rc)
     assert ws.bands_intact()
+    assert L.nf4_gemm_check_workspace(ws.ptr() if wsz else None, wsz, _stream()) == 0
     if wsz:
         assert int(ws.body().count_nonzero()) == 0  # tickets and slab entries back at 0
     for N, gp, ga1, ga2, y, (p, a1, a2) in keep:

@@ -12,11 +12,21 @@
 //   ABL_NOSCALE register-resident kernel: no absmax byte / nested scale gathers
 //   ABL_NORING  ABL_NOWLOAD + ABL_NOSCALE: the ring issues no memory operation
 //   ABL_L2WIN   weight loads folded into a 256 KiB window (L2-resident, same instructions)
+//   ABL_DROPSLICE  128-deep kernel: K slice 1 withholds its split-K partials (takes its
+//               ticket all the same), so the reducer's bounded poll gives up: proves the
+//               workspace error word fires (tools/splitk_timeout_probe.py, one run)
 #include <hip/hip_runtime.h>
+
+#if defined(ABL_DROPSLICE)
+#define NF4_ABL_KEEP_SLICE(ks_) ((ks_) != 1u)
+#endif
 
 #if defined(ABL_NORING)  // no memory traffic in the ring at all
 #define ABL_NOWLOAD
 #define ABL_NOSCALE
+#endif
+#if defined(ABL_NOWLOAD) || defined(ABL_NOSCALE)  // the ring issues fewer loads per slot
+#define NF4_ABL_RING_FULL 0
 #endif
 #if defined(ABL_NOLUT)
 #define NF4_ABL_LOOKUP(pt_, addr_, wd_) \

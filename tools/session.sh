@@ -62,6 +62,18 @@ for stage in "$@"; do
         cat "$O/gemm_stamps.jsonl" ;;
     dqab)  # interleaved dequant launch-config A/B: DQAB_ARGS passed to tools/dq_ab.py
         timeout -k 10 400 $PY tools/dq_ab.py ${DQAB_ARGS:-} > "$O/dq_ab.jsonl" 2> "$O/dq_ab.err"; cat "$O/dq_ab.jsonl" ;;
+    cacheab)  # independent input / output rotation (tools/cache_ab.py): CACHEAB_RUNS="tag|args;tag|args"
+        IFS=';' read -ra RS <<< "${CACHEAB_RUNS:-bf16|}"
+        for kv in "${RS[@]}"; do
+            timeout -k 10 300 $PY tools/cache_ab.py --tag "${kv%%|*}" ${kv#*|} >> "$O/cache_ab.jsonl" 2>> "$O/cache_ab.err"
+        done
+        cat "$O/cache_ab.jsonl" ;;
+    tprobe)  # split-K timeout is reported (tools/_build/libnf4dq_abl_dropslice.so, built here): ONE run
+        test -f tools/_build/libnf4dq_abl_dropslice.so
+        NF4DQ_LIB_PATH=tools/_build/libnf4dq_abl_dropslice.so timeout -k 10 120 $PY tools/splitk_timeout_probe.py \
+            > "$O/splitk_timeout_probe.jsonl" 2> "$O/tprobe.err"
+        timeout -k 10 120 $PY tools/splitk_timeout_probe.py >> "$O/splitk_timeout_probe.jsonl" 2>> "$O/tprobe.err"
+        cat "$O/splitk_timeout_probe.jsonl" ;;
     gemmab)  # decode GEMM per launch, product vs the A/B libraries named in ABLIBS (tools/_build/libnf4dq_<x>.so)
         timeout -k 10 300 $PY tools/gemm_ab.py ${GEMMAB_ARGS:-} >> "$O/gemm_ab.jsonl" 2>> "$O/gemm_ab.err"
         for x in ${ABLIBS:-}; do

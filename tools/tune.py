@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--tiles", default="4")
     ap.add_argument("--bpcu", default="0,1,2,4,8")
     ap.add_argument("--nt", default="1")
-    ap.add_argument("--flags", default="0", help="NF4DQ_CFG_A1_PREFETCH field: (log2 tiles) << 8, 0 = off")
+    ap.add_argument("--flags", default="0", help="nf4_launch_cfg.flags: reserved, must be 0 (kept for old logs)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     m, n, P = args.m, args.n, args.sets
