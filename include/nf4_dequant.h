@@ -183,7 +183,7 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
  * (1 = no cross-workgroup reduction). */
 #define NF4DQ_GEMM_XR 5
 /* NF4DQ_GEMM_SK: balanced ("stream-K") kernel (K % 256 == 0, M K 2 <= 64 KiB):
- * one workgroup of `waves` (16) waves per CU, the (16-column strip, 256-deep
+ * one workgroup of `waves` (8) waves per CU, the (16-column strip, 256-deep
  * chunk) units of the launch split evenly over the waves, x[M][K] in LDS;
  * strips shared by neighbouring workgroups meet in the split-K slab.  depth and
  * strips are ignored, ksplit must be 1.  Needs at least one unit per CU and at

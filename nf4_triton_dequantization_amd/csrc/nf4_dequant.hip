@@ -82,7 +82,7 @@ struct Batch {
 #define NF4_FSTAMP(slot_, val_)                                                                      \
     do {                                                                                             \
         __builtin_amdgcn_sched_barrier(0);                                                           \
-        if (lane == 0) bt.stamps[(blockIdx.x * kWaves + (threadIdx.x >> 6)) * 4u + (slot_)] = (val_); \
+        if (lane == 0) bt.stamps[(blockIdx.x * kFlatWaves + (threadIdx.x >> 6)) * 4u + (slot_)] = (val_); \
         __builtin_amdgcn_sched_barrier(0);                                                           \
     } while (0)
 #define NF4_FNOW() __builtin_amdgcn_s_memrealtime()
@@ -105,15 +105,47 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
     }
 }
 
-constexpr int kWg = 256;   // 4 waves per workgroup (every kernel here)
-constexpr int kWaves = 4;
-constexpr int kU = 4;      // packed dwords (fp32 output: words) per lane per tile
+// Variant hooks of the flat kernel: the product values by default.  tools/dq_variants.hip
+// redefines them to build A/B libraries (tools/_build/libnf4dq_dqv_<x>.so, timing in the
+// HBM-streamed regime with tools/cache_ab.py --libs); nothing in the product sets them.
+//   NF4_DQ_FLAT_WAVES   waves per workgroup of the flat kernel (4)
+//   NF4_DQ_U            packed dwords per lane per tile (4: 1 KiB of packed bytes per wave)
+//   NF4_DQ_AUX_STORE    cache-policy bits of the output stores (18 = sc1 + nt)
+//   NF4_DQ_AUX_LOAD     cache-policy bits of the packed-weight loads (2 = nt)
+//   NF4_DQ_SCALE_FIRST  1: a tile's absmax / nested-scale loads go out before its packed loads
+#ifndef NF4_DQ_FLAT_WAVES
+#define NF4_DQ_FLAT_WAVES 4
+#endif
+#ifndef NF4_DQ_U
+#define NF4_DQ_U 4
+#endif
+#ifndef NF4_DQ_AUX_STORE
+#define NF4_DQ_AUX_STORE 18
+#endif
+#ifndef NF4_DQ_AUX_LOAD
+#define NF4_DQ_AUX_LOAD 2
+#endif
+#ifndef NF4_DQ_SCALE_FIRST
+#define NF4_DQ_SCALE_FIRST 0
+#endif
+
+constexpr int kWg = 256;   // rows / bitsandbytes-bytes kernels: 4 waves per workgroup
+constexpr int kFlatWaves = NF4_DQ_FLAT_WAVES;  // the flat kernel's workgroup
+constexpr int kFlatWg = 64 * kFlatWaves;
+constexpr int kU = NF4_DQ_U;  // packed dwords (fp32 output: words) per lane per tile
 
 // Cache-policy bits of the buffer instructions (aux operand, gfx950 CPol):
 // 2 = nt (streaming), 16 = sc1.  Output stores are sc1+nt: a write-once stream,
 // not kept in the XCD L2 (+25-30 % over default-policy stores, and 1-2 % over nt
 // alone; profiles/r01/tune_sweep.log).
-constexpr int kAuxStore = 18;
+constexpr int kAuxStore = NF4_DQ_AUX_STORE;
+// Packed-weight loads are nt (streaming; round 4): a streamed model reads each weight
+// once, from HBM.  With the default policy a 4096^2 launch whose weights come from
+// HBM takes 7.95 us (66 %); with nt loads 7.46-7.49 us (70-71 %), the same whether or
+// not the weights are still in the Infinity Cache (nt reads do not use it: the
+// cache-warm figure becomes 7.45 instead of 6.86 us).  Sc0 / sc1 bits beside nt
+// change nothing (profiles/r04/cache/dequant_variants_4096.jsonl).
+constexpr int kAuxLoad = NF4_DQ_AUX_LOAD;
 
 template <int DT>
 constexpr uint32_t out_bytes_per_packed_byte() { return DT == NF4DQ_F32 ? 8u : 4u; }
@@ -150,15 +182,18 @@ template <int DT, int MODE>
 __device__ __forceinline__ TileIn tile_load(const Desc& D, __amdgpu_buffer_rsrc_t rp, uint32_t base, uint32_t lane) {
     constexpr uint32_t LB = lane_bytes<DT>();
     TileIn in;
+    auto packed_loads = [&]() {
 #pragma unroll
-    for (int j = 0; j < kU; ++j) {
-        const uint32_t off = base + 64u * LB * j + LB * lane;
-        if constexpr (LB == 4) {
-            in.w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, 0);
-        } else {
-            in.w[j] = __builtin_amdgcn_raw_buffer_load_b16(rp, off, 0, 0);
+        for (int j = 0; j < kU; ++j) {
+            const uint32_t off = base + 64u * LB * j + LB * lane;
+            if constexpr (LB == 4) {
+                in.w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, off, 0, kAuxLoad);
+            } else {
+                in.w[j] = __builtin_amdgcn_raw_buffer_load_b16(rp, off, 0, kAuxLoad);
+            }
         }
-    }
+    };
+    if constexpr (!NF4_DQ_SCALE_FIRST) packed_loads();
     const uint32_t g = tile_block<DT>(D, base, lane);
     if constexpr (MODE == kRef) {
         in.a1 = D.a1[fmodu(g, D.nb)];
@@ -175,6 +210,7 @@ __device__ __forceinline__ TileIn tile_load(const Desc& D, __amdgpu_buffer_rsrc_
     } else {
         in.a2 = D.a2[g];
     }
+    if constexpr (NF4_DQ_SCALE_FIRST) packed_loads();
     return in;
 }
 
@@ -264,7 +300,7 @@ __device__ __forceinline__ void make_rsrcs(const Batch<MAXB>& bt, uint32_t k, __
 // loads are in flight while tile i is decoded and stored, with no register copies
 // (a copy would force a wait on the loads it copies).
 template <int DT, int MODE, int MAXB>
-__global__ __launch_bounds__(kWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
+__global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
     __shared__ __attribute__((aligned(16))) float lut[16];
     __shared__ __attribute__((aligned(16))) float code2s[MODE == kBnb ? 256 : 1];  // bitsandbytes code (every piece's)
     const uint32_t lane = threadIdx.x & 63u;
@@ -272,8 +308,8 @@ __global__ __launch_bounds__(kWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
     const unsigned long long t_entry = NF4_FNOW();
     unsigned long long tiles_done = 0;
 #endif
-    const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
-    const uint32_t nwaves = gridDim.x * kWaves;
+    const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kFlatWaves + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * kFlatWaves;
 
     // First tile's loads go out before anything else (a wave without work
     // issues them past the buffer range: no traffic); the LUT write and the
@@ -292,7 +328,7 @@ __global__ __launch_bounds__(kWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
     }
     write_lut(lut);
     if constexpr (MODE == kBnb) {  // every piece of a bitsandbytes stream carries the same code
-        for (uint32_t i = threadIdx.x; i < 256u; i += kWg) code2s[i] = bt.d[0].code2[i];
+        for (uint32_t i = threadIdx.x; i < 256u; i += kFlatWg) code2s[i] = bt.d[0].code2[i];
     }
     __syncthreads();
     if (!ca.valid) {
@@ -428,7 +464,7 @@ int cu_count() {
 
 template <int DT, int MODE, int MAXB>
 void launch_one(const Batch<MAXB>& b, uint64_t blocks, hipStream_t st) {
-    hipLaunchKernelGGL((nf4_flat_kernel<DT, MODE, MAXB>), dim3((unsigned)blocks), dim3(kWg), 0, st, b);
+    hipLaunchKernelGGL((nf4_flat_kernel<DT, MODE, MAXB>), dim3((unsigned)blocks), dim3(kFlatWg), 0, st, b);
 }
 
 // Launch one flat batch.  Tile offsets are (re)computed here for the tile size of
@@ -446,7 +482,7 @@ int launch_flat_batch(const Batch<MAXB>& bt, int dtype, int mode, const nf4_laun
     }
     b.total_tiles = acc;
     if (acc == 0) return NF4DQ_OK;
-    uint64_t blocks = (acc + kWaves - 1) / kWaves;
+    uint64_t blocks = (acc + kFlatWaves - 1) / kFlatWaves;
     if (cfg.blocks_per_cu > 0) {
         const uint64_t cap = (uint64_t)cfg.blocks_per_cu * (uint64_t)cu_count();
         if (blocks > cap) blocks = cap;

@@ -1859,6 +1859,8 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
 //    workgroup order (splitk_reduce): one launch, bitwise reproducible.
 //  * Dequant + MFMA per unit: the streaming kernels' pair-table body (sslot_mma),
 //    x[M][K] staged once per workgroup in LDS.
+//  * 8 waves per workgroup (2 per SIMD, up to 256 registers): a wave's units all
+//    in flight at once (up to 8 x 2 KiB), no register-capped drain.
 struct SkArgs {
     StreamMat mat[kGroupMax];
     uint32_t nmat;
@@ -1870,19 +1872,20 @@ struct SkArgs {
     FastDiv ppr;         // 16-byte x pieces per row (K / 8)
     uint32_t U;          // units: strips x C
     uint32_t GW;         // waves in the grid
+    FastDiv fGW, fU;     // division by GW and by U (host: U * GW < 2^31)
     uint32_t ncols;      // sum of N (slab row length)
     uint32_t bpr, groups;
     uint32_t xstride;    // LDS bytes per staged x row (16-B padded: rows 4 banks apart)
     uint32_t zero_off;   // 128 zero bytes: the A operand of rows >= M
 };
 
-// First unit of grid wave g (g = GW: one past the last)
-__device__ __forceinline__ uint32_t sk_u0(const SkArgs& A, uint32_t g) {
-    return (uint32_t)(((uint64_t)g * A.U) / A.GW);
-}
-// The grid wave whose range holds unit u (the largest g with sk_u0(g) <= u)
+// First unit of grid wave g (g = GW: one past the last) = floor(g U / GW): the units
+// spread evenly, a wave's range differs from any other's by at most one unit.  32-bit
+// (host: U GW < 2^31), multiply-high division.
+__device__ __forceinline__ uint32_t sk_u0(const SkArgs& A, uint32_t g) { return fdiv(g * A.U, A.fGW); }
+// The grid wave whose range holds unit u: the largest g with sk_u0(g) <= u
 __device__ __forceinline__ uint32_t sk_wave_of(const SkArgs& A, uint32_t u) {
-    return (uint32_t)((((uint64_t)u + 1u) * A.GW - 1u) / A.U);
+    return fdiv((u + 1u) * A.GW - 1u, A.fU);
 }
 // The weight of a launch-wide strip (straight-line selects, uniform)
 __device__ __forceinline__ uint32_t sk_mat_of(const SkArgs& A, uint32_t strip) {
@@ -1898,7 +1901,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_sk_kernel(const SkArgs A) {
     __shared__ __attribute__((aligned(16))) f32x2 ptab[256 * 32];
     __shared__ float qtab[256];
     __shared__ uint32_t wrange[W][2];  // each wave's [first unit, units)
-    constexpr int D = LM < 4 ? LM : 4;  // ring depth: 4 x 2 KiB per wave, 16 waves = 128 KiB in flight per CU
+    constexpr int D = LM < 8 ? LM : 8;  // ring depth: up to 8 x 2 KiB per wave, 8 waves = 128 KiB in flight per CU
     constexpr int XP = 4096 / (64 * W);  // 16-byte x pieces per thread: 64 KiB of x at most
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2200,7 +2203,7 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
     if (c.kernel == NF4DQ_GEMM_SK) {
         // static rules only: whether the launch's column total spreads over the CUs is
         // checked at launch (sk_plan; a grouped launch counts every weight's columns)
-        return K % kSChunkK == 0 && M * K * 2 <= 65536 && c.waves == 16 && c.ksplit == 1;
+        return K % kSChunkK == 0 && M * K * 2 <= 65536 && c.waves == 8 && c.ksplit == 1;
     }
     if (c.kernel == NF4DQ_GEMM_XS) {
         if (c.waves != 4 && c.waves != 8) return false;
@@ -2650,7 +2653,7 @@ static int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, i
     return hip_rc2(hipGetLastError());
 }
 
-// Balanced kernel plan (nf4_gemm_sk_kernel): one workgroup of 16 waves per CU,
+// Balanced kernel plan (nf4_gemm_sk_kernel): one workgroup of 8 waves per CU,
 // units = strips x (K / 256) split evenly over the waves.  Runs when x fits its
 // LDS (M K 2 <= 64 KiB), every workgroup gets a unit, and a wave's range is at
 // most one strip and 16 units long.  `slots`: most workgroups sharing one strip
@@ -2659,17 +2662,22 @@ struct SkPlan {
     uint32_t G, W, GW, C, LM, slots, xstride, zero_off, lds;
     uint64_t U;
 };
+// static LDS of nf4_gemm_sk_kernel<., 8, .>: pair table, q/127 table, the waves' ranges;
+// the opt-in cap must keep static + dynamic within the CU's 160 KiB (an attribute
+// request beyond it fails, and its error would be the launch's hipGetLastError)
+constexpr uint32_t kSkStatic = kStreamStatic + 8u * 2u * 4u;
+constexpr uint32_t kSkLdsCap = kLdsPerCu - kSkStatic;
 
 static bool sk_plan(int64_t M, int64_t K, int64_t ncols, int waves, SkPlan& p) {
     if (M < 1 || M > 16 || K <= 0 || K % kSChunkK || M * K * 2 > 65536 || ncols <= 0 || ncols % 16) return false;
-    if (waves != 16) return false;
+    if (waves != 8) return false;
     p.W = (uint32_t)waves;
     p.G = (uint32_t)device_cus();
     p.GW = p.G * p.W;
     p.C = (uint32_t)(K / kSChunkK);
     const uint64_t strips = (uint64_t)ncols / 16u;
     p.U = strips * p.C;
-    if (p.U >= (uint64_t(1) << 31) || p.U < p.G) return false;  // every workgroup gets >= 1 unit
+    if (p.U < p.G) return false;  // every workgroup gets >= 1 unit
     const uint64_t L = (p.U + p.GW - 1) / p.GW;                 // longest wave range
     if (L > p.C) return false;                                  // <= one strip: two partial tiles at most
     uint32_t lm = 1;
@@ -2677,7 +2685,8 @@ static bool sk_plan(int64_t M, int64_t K, int64_t ncols, int waves, SkPlan& p) {
     if (lm > 16) return false;
     p.LM = lm;
     const uint64_t GW = p.GW, U = p.U;
-    auto wg_of = [&](uint64_t u) { return ((u + 1) * GW - 1) / U / p.W; };
+    if (U * GW >= (uint64_t(1) << 31)) return false;  // the device's 32-bit range math
+    auto wg_of = [&](uint64_t u) { return ((u + 1) * GW - 1) / U / p.W; };  // sk_wave_of / W
     uint64_t slots = 1;
     for (uint64_t s = 0; s < strips; ++s) {
         const uint64_t a = wg_of(s * p.C), b = wg_of(s * p.C + p.C - 1);
@@ -2688,7 +2697,7 @@ static bool sk_plan(int64_t M, int64_t K, int64_t ncols, int waves, SkPlan& p) {
     p.zero_off = (uint32_t)M * p.xstride;
     const uint32_t xb = p.zero_off + 128u, rb = p.W * 2u * 64u * 16u;
     p.lds = xb > rb ? xb : rb;
-    return p.lds + kStreamStatic + 2u * 4u * p.W <= kLdsPerCu;
+    return p.lds <= kSkLdsCap;
 }
 
 static size_t sk_workspace(int64_t M, int64_t K, int64_t ncols, int waves) {
@@ -2716,6 +2725,8 @@ static int launch_sk(const HostMat* mats, int count, const void* x, int64_t M, i
     A.ppr = make_fastdiv((uint32_t)(K / 8));
     A.U = (uint32_t)p.U;
     A.GW = p.GW;
+    A.fGW = make_fastdiv(p.GW);
+    A.fU = make_fastdiv((uint32_t)p.U);
     A.ncols = (uint32_t)ncols;
     A.bpr = (uint32_t)(K / 64);
     A.groups = (A.bpr + 3) / 4;
@@ -2745,11 +2756,11 @@ static int launch_sk(const HostMat* mats, int count, const void* x, int64_t M, i
     do {                                                                                                   \
         static bool attr_ = false; /* static + dynamic LDS above 64 KiB needs the opt-in */                \
         if (!attr_) {                                                                                      \
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_sk_kernel<DT_, 16, LM_>),    \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStreamLdsCap);     \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_sk_kernel<DT_, 8, LM_>),    \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSkLdsCap);         \
             attr_ = true;                                                                                  \
         }                                                                                                  \
-        hipLaunchKernelGGL((nf4_gemm_sk_kernel<DT_, 16, LM_>), grid, block, p.lds, st, A);                 \
+        hipLaunchKernelGGL((nf4_gemm_sk_kernel<DT_, 8, LM_>), grid, block, p.lds, st, A);                 \
     } while (0)
 #define NF4_SKL(DT_)                          \
     do {                                      \

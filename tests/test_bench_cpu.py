@@ -56,6 +56,10 @@ def test_gpus_flag_spawns_ranks(n):
     per_matrix = 64 * 128 // 64 + 4 * ((64 * 128 // 64 + 255) // 256)
     assert c5["quant_state_bytes_per_rank"] == [per_matrix * len(range(r, 8, n)) for r in range(n)]
     assert c5["verified_first_rows"] is True
+    # the rotation each rank ran is on the line (headline and c5): sets and distinct bytes
+    for reg in (d["config"]["rotation"], c5["regime"]):
+        assert reg["in_sets"] >= 1 and reg["out_sets"] >= 1
+        assert reg["read_footprint_bytes"] > 0 and reg["write_footprint_bytes"] > 0 and reg["weights_from"]
     assert c5["cpu_baseline"]["native"] > 0 and c5["cpu_baseline"]["value"] > 0
 
 
@@ -97,3 +101,26 @@ def test_c5_partition_covers_every_matrix_once():
         assert ids == list(range(8))
         sizes = [len(bench.rank_matrices(a, r, world)) for r in range(world)]
         assert sizes == [8 // world] * world
+
+
+def test_rotation_streams_weights_from_hbm_at_every_n():
+    """every rank's rotation reads >= 512 MiB of distinct weight bytes
+    (2x the 256 MiB Infinity Cache, where the launch time stops depending on the
+    rotation: profiles/r04/cache/cache_ab_4096.jsonl) and writes >= 512 MiB, so the
+    headline and the c5 object at N = 1, 2, 4, 8 all see the same HBM-streamed regime."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    pin, pout = bench.rotation_sets([(0, 4096, 4096)])
+    rd, wr = bench.step_bytes([(0, 4096, 4096)])
+    assert (pin, pout) == (63, 16)
+    assert pin * rd >= 512 << 20 and pout * wr >= 512 << 20
+    for world in (1, 2, 4, 8):
+        a = bench.parse_args(["--workload", "c5", "--gpus", str(world)])
+        for r in range(world):
+            mats = bench.rank_matrices(a, r, world)
+            pin, pout = bench.rotation_sets(mats)
+            rd, wr = bench.step_bytes(mats)
+            assert pin * rd >= bench.MIN_READ_FOOTPRINT and pout * wr >= bench.MIN_WRITE_FOOTPRINT
+            # the smallest rotation that does it (no needless memory)
+            assert (pin - 1) * rd < bench.MIN_READ_FOOTPRINT or pin == 1

@@ -745,7 +745,7 @@ def _sk_call(L, _lib, x, mats, dt_code, K):
     import ctypes
 
     M = x.shape[0]
-    cfg = _lib.GemmCfg(_lib.GEMM_SK, 16, 0, 1, 0)
+    cfg = _lib.GemmCfg(_lib.GEMM_SK, 8, 0, 1, 0)
     arr = (_lib.GemmMat * len(mats))()
     for i, (p, a1, a2, y) in enumerate(mats):
         arr[i] = _lib.GemmMat(p.data_ptr(), p.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
@@ -806,7 +806,7 @@ def test_balanced_kernel_rejects_what_it_cannot_spread(gpu):
 
     L = _lib.lib()
     F = 0x1000
-    c = _lib.GemmCfg(_lib.GEMM_SK, 16, 0, 1, 0)
+    c = _lib.GemmCfg(_lib.GEMM_SK, 8, 0, 1, 0)
     for (M, N, K) in [(1, 64, 2048), (9, 4096, 4096), (1, 4096, 1152), (33, 4096, 4096)]:
         rc = L.nf4_gemm_ref_cfg(F, M, F, N * K // 2, F, N * K // 64, F, 16, F, _lib.BF16, N, K, F, 1 << 30,
                                 ctypes.byref(c), None)

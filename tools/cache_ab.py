@@ -1,7 +1,7 @@
 """Where do the headline's reads come from?  Independent input / output rotation A/B.
 
     python tools/cache_ab.py [--shape 4096x4096] [--dtype bf16|f32]
-                             [--pairs 13x13,40x13,13x60,...] [--rounds 5] [--steps 128]
+                             [--pairs 13x13,40x13,13x60@4,...] [--rounds 5] [--steps 128]
 
 Step i of a configuration ``IxO`` reads input set ``i % I`` (packed weight + absmax +
 nested absmax) and writes output set ``i % O``, so the distinct *read* bytes
@@ -11,6 +11,11 @@ output sets is slow while the converse is fast, the per-launch time depends on
 whether the packed weights stay in the 256 MiB Infinity Cache (the nt output stores
 not displacing them); if the converse holds, on how much address space the
 rotation walks (translation reach).  VERDICT r03 "Next round" item 1.
+``IxO@b`` times launch configuration blocks_per_cu = b (nf4_dequant_ref_cfg; the
+library default, b = 0, otherwise): the launch knobs re-checked in the regime
+where the weights stream from HBM.  ``--libs a.so,b.so``: every configuration is
+also timed through each of these builds of the C ABI (tools/dq_variants.hip A/B
+libraries), loaded side by side in this process and interleaved with the product.
 
 Timing as bench.py: one untimed pass over every set of a configuration, a device
 spin covering the host's submission, 16 untimed lead launches, K eager launches
@@ -49,8 +54,15 @@ def main():
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--lead", type=int, default=16)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--libs", default="", help="extra builds of the C ABI to time beside the product")
     args = ap.parse_args()
-    L = _lib.lib()
+    libs = [("prod", _lib.lib())]
+    for path in [v for v in args.libs.split(",") if v]:
+        h = ctypes.CDLL(os.path.abspath(path))
+        for name, (res_t, argt) in _lib.SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype, fn.argtypes = res_t, argt
+        libs.append((os.path.basename(path).replace("libnf4dq_", "").replace(".so", ""), h))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     st = torch.cuda.current_stream()
@@ -61,7 +73,11 @@ def main():
     nbytes, nb = m * n // 2, m * n // 64
     n2 = (nb + 255) // 256
     alg = W.algorithmic_bytes(m, n, ob, nb, n2)
-    pairs = [tuple(int(v) for v in p.split("x")) for p in args.pairs.split(",")]
+    pairs = []
+    for p in args.pairs.split(","):
+        io, _, b = p.partition("@")
+        for li in range(len(libs)):
+            pairs.append(tuple(int(v) for v in io.split("x")) + (int(b or 0), li))
     I_max = max(p[0] for p in pairs)
     O_max = max(p[1] for p in pairs)
 
@@ -75,10 +91,17 @@ def main():
 
     sp = st.cuda_stream
 
-    def launch(i, I, O):
+    cfgs = {b: _lib.LaunchCfg(4, b, 1, 0) for b in {p[2] for p in pairs}}
+
+    def launch(i, I, O, b=0, li=0):
+        L = libs[li][1]
         q, a1, a2 = ins[i % I]
-        rc = L.nf4_dequant_ref(q.data_ptr(), nbytes, a1.data_ptr(), nb, a2.data_ptr(), n2,
-                               outs[i % O].data_ptr(), code, m, n, sp)
+        if b:
+            rc = L.nf4_dequant_ref_cfg(q.data_ptr(), nbytes, a1.data_ptr(), nb, a2.data_ptr(), n2,
+                                       outs[i % O].data_ptr(), code, m, n, ctypes.byref(cfgs[b]), sp)
+        else:
+            rc = L.nf4_dequant_ref(q.data_ptr(), nbytes, a1.data_ptr(), nb, a2.data_ptr(), n2,
+                                   outs[i % O].data_ptr(), code, m, n, sp)
         if rc:
             raise RuntimeError(_lib.strerror(rc))
 
@@ -90,41 +113,47 @@ def main():
     cyc_per_us = 2_000_000 / max(e0.elapsed_time(e1) * 1e3, 1.0)
 
     # touch every set once (TLB-warm, as resident weights are)
-    for i in range(max(I_max, O_max)):
-        launch(i, I_max, O_max)
+    for li in range(len(libs)):
+        for i in range(max(I_max, O_max)):
+            launch(i, I_max, O_max, 0, li)
     torch.cuda.synchronize()
     res = {p: [] for p in pairs}
     for _ in range(args.rounds):
-        for (I, O) in pairs:
+        for (I, O, b, li) in pairs:
             for i in range(max(I, O)):  # the configuration's own untimed pass
-                launch(i, I, O)
+                launch(i, I, O, b, li)
             torch.cuda._sleep(int(cyc_per_us * (30.0 * (args.steps + args.lead) + 200.0)))
             for j in range(args.lead):
-                launch(j - args.lead + 10 * I * O, I, O)
+                launch(j - args.lead + 10 * I * O, I, O, b, li)
             e0.record(st)
             for i in range(args.steps):
-                launch(i, I, O)
+                launch(i, I, O, b, li)
             e1.record(st)
             torch.cuda.synchronize()
-            res[(I, O)].append(e0.elapsed_time(e1) * 1e3 / args.steps)
+            res[(I, O, b, li)].append(e0.elapsed_time(e1) * 1e3 / args.steps)
     # hygiene: set 0's output vs the oracle (first 32 rows)
     import nf4_oracle as Ora
 
-    launch(0, 1, 1)
-    torch.cuda.synchronize()
     r = 32
-    if args.dtype != "f32":
-        want = Ora.dequant_ref_np(p0[: r * n // 2], a10, a20, r, n, Ora.BF16 if args.dtype == "bf16" else Ora.F16)
-        got = outs[0][:r].contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
-        ok = bool(np.array_equal(got, want))
-    else:
-        ok = None
-    for (I, O) in pairs:
-        ts = sorted(res[(I, O)])
+    oks = []
+    for li in range(len(libs)):
+        outs[0].zero_()
+        launch(0, 1, 1, 0, li)
+        torch.cuda.synchronize()
+        if args.dtype != "f32":
+            want = Ora.dequant_ref_np(p0[: r * n // 2], a10, a20, r, n, Ora.BF16 if args.dtype == "bf16" else Ora.F16)
+            got = outs[0][:r].contiguous().view(torch.int16).cpu().numpy().view(np.uint16)
+            oks.append(bool(np.array_equal(got, want)))
+        else:
+            oks.append(None)
+    for (I, O, b, li) in pairs:
+        ok = oks[li]
+        ts = sorted(res[(I, O, b, li)])
         med = ts[len(ts) // 2]
         rd = I * (nbytes + nb + 4 * n2)
         wr = O * m * n * ob
         print(json.dumps({"tag": args.tag, "m": m, "n": n, "dtype": args.dtype, "in_sets": I, "out_sets": O,
+                          "blocks_per_cu": b, "lib": libs[li][0],
                           "read_MB": round(rd / 1e6, 1), "written_MB": round(wr / 1e6, 1),
                           "footprint_MB": round((rd + wr) / 1e6, 1),
                           "us_median": round(med, 3), "us_min": round(ts[0], 3), "us_max": round(ts[-1], 3),

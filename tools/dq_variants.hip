@@ -1,0 +1,29 @@
+// A/B variants of the flat dequant kernel (tools only; never in the product library).
+// Sets the NF4_DQ_* hooks of nf4_dequant.hip from -DDQV_* values and includes the
+// product source; tools/Makefile `dqv` builds one library per named variant (its
+// DQV flags in the Makefile's table), linked with tools/gemm_stub.cpp (the GEMM entry
+// points as ERR_ARG stubs, so a variant library stays small) and the product's
+// host-CPU object into tools/_build/libnf4dq_dqv_<name>.so, timed against the
+// product by tools/cache_ab.py --libs in the regime where the weights stream from HBM.
+//   DQV_WG=n   waves per workgroup (product 4)
+//   DQV_U=n    packed dwords per lane per tile (product 4)
+//   DQV_LD=p   cache-policy bits of the packed-weight loads (product 2 = nt; 16 = sc1, 1 = sc0, 0 = default)
+//   DQV_ST=p   cache-policy bits of the output stores (product 18 = sc1 + nt)
+//   DQV_SF=1   a tile's scale loads issued before its packed loads
+#ifdef DQV_WG
+#define NF4_DQ_FLAT_WAVES DQV_WG
+#endif
+#ifdef DQV_U
+#define NF4_DQ_U DQV_U
+#endif
+#ifdef DQV_LD
+#define NF4_DQ_AUX_LOAD DQV_LD
+#endif
+#ifdef DQV_ST
+#define NF4_DQ_AUX_STORE DQV_ST
+#endif
+#ifdef DQV_SF
+#define NF4_DQ_SCALE_FIRST DQV_SF
+#endif
+
+#include "../nf4_triton_dequantization_amd/csrc/nf4_dequant.hip"
