@@ -61,4 +61,11 @@
 #define NF4_ABL_HANDOFF_ON 0
 #endif
 
+// the product's fused-GEMM sources, all in this one translation unit
 #include "../nf4_triton_dequantization_amd/csrc/nf4_gemm.hip"
+#include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_k128.hip"
+#include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_persist.hip"
+#include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_sk.hip"
+#include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_stream.hip"
+#include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_xr.hip"
+#include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_xs.hip"

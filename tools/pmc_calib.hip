@@ -8,7 +8,8 @@
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Reads `nbytes` with 4 B/lane buffer_load_dword, 256 contiguous bytes per wave
-// instruction (the packed-weight load shape); writes one dword per wave.
+// instruction, nt policy (the packed-weight load shape and policy, round 4); writes one
+// dword per wave.
 __global__ __launch_bounds__(256) void calib_read_dword(const uint32_t* p, uint32_t nbytes, uint32_t* sink) {
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, nbytes, 0x00020000);
     const uint32_t lane = threadIdx.x & 63u;
@@ -17,7 +18,7 @@ __global__ __launch_bounds__(256) void calib_read_dword(const uint32_t* p, uint3
     uint32_t acc = 0;
     for (uint32_t base = wave * 2048u; base < nbytes; base += nw * 2048u) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc ^= __builtin_amdgcn_raw_buffer_load_b32(r, base + 256u * j + 4u * lane, 0, 0);
+        for (int j = 0; j < 8; ++j) acc ^= __builtin_amdgcn_raw_buffer_load_b32(r, base + 256u * j + 4u * lane, 0, 2);
     }
     if (acc == 0x9E3779B9u) sink[wave] = acc;  // practically never: keeps the loads alive
 }
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(256) void calib_mix(const uint32_t* p, uint32_t nby
     for (uint32_t base = wave * 1024u; base < nbytes; base += nw * 1024u) {
         uint32_t w[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, base + 256u * j + 4u * lane, 0, 0);
+        for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, base + 256u * j + 4u * lane, 0, 2);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const u32x4 v = {w[j], w[j] ^ 1u, w[j] ^ 2u, w[j] ^ 3u};

@@ -3,8 +3,9 @@
 1. calibration: calib_read (1 GiB, 4 B/lane dword loads) and calib_write (1 GiB,
    16 B/lane nt stores) x 4 each -- known byte counts in the dequant kernel's
    two access shapes;
-2. the bench workload: 4096x4096 NF4->bf16 dequant over 16 rotating buffer sets,
-   48 launches with bench.py's default launch config.
+2. the bench workload: 4096x4096 NF4->bf16 dequant, bench.py's rotation (round 4:
+   input and output sets rotated independently, >= 512 MiB of distinct reads and of
+   writes, so the weights stream from HBM), 96 launches of the product entry.
 """
 import ctypes
 import os
@@ -37,20 +38,21 @@ def main():
     del buf
     nb = m * n // 64
     n2 = (nb + 255) // 256
-    sets = []
+    sys.path.insert(0, REPO)
+    import bench
+
+    pin, pout = bench.rotation_sets([(0, m, n)])
     g = torch.Generator(device=dev)
     g.manual_seed(1)
-    for _ in range(16):
-        sets.append((torch.randint(0, 256, (m * n // 2,), dtype=torch.uint8, device=dev, generator=g),
-                     torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=g),
-                     torch.rand(n2, device=dev, generator=g) * 0.01,
-                     torch.empty((m, n), dtype=torch.bfloat16, device=dev)))
-    cfg = _lib.LaunchCfg(4, 0, 1, 0)  # bench.py defaults
+    ins = [(torch.randint(0, 256, (m * n // 2,), dtype=torch.uint8, device=dev, generator=g),
+            torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=g),
+            torch.rand(n2, device=dev, generator=g) * 0.01) for _ in range(pin)]
+    outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(pout)]
     L = _lib.lib()
-    for i in range(48):
-        q, a1, a2, out = sets[i % 16]
-        assert L.nf4_dequant_ref_cfg(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
-                                     out.data_ptr(), _lib.BF16, m, n, ctypes.byref(cfg), st) == 0
+    for i in range(96):
+        q, a1, a2 = ins[i % pin]
+        assert L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                                 outs[i % pout].data_ptr(), _lib.BF16, m, n, st) == 0
     torch.cuda.synchronize()
     print("pmc probe done", m, n)
 
