@@ -113,6 +113,7 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 //   NF4_DQ_AUX_STORE    cache-policy bits of the output stores (18 = sc1 + nt)
 //   NF4_DQ_AUX_LOAD     cache-policy bits of the packed-weight loads (2 = nt)
 //   NF4_DQ_SCALE_FIRST  1: a tile's absmax / nested-scale loads go out before its packed loads
+//   NF4_DQ_SCALE_NT     1: the absmax / nested-scale gathers carry the nt policy too
 #ifndef NF4_DQ_FLAT_WAVES
 #define NF4_DQ_FLAT_WAVES 4
 #endif
@@ -127,6 +128,9 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #endif
 #ifndef NF4_DQ_SCALE_FIRST
 #define NF4_DQ_SCALE_FIRST 0
+#endif
+#ifndef NF4_DQ_SCALE_NT
+#define NF4_DQ_SCALE_NT 0
 #endif
 
 constexpr int kWg = 256;   // rows / bitsandbytes-bytes kernels: 4 waves per workgroup
@@ -196,10 +200,17 @@ __device__ __forceinline__ TileIn tile_load(const Desc& D, __amdgpu_buffer_rsrc_
     if constexpr (!NF4_DQ_SCALE_FIRST) packed_loads();
     const uint32_t g = tile_block<DT>(D, base, lane);
     if constexpr (MODE == kRef) {
-        in.a1 = D.a1[fmodu(g, D.nb)];
         const uint32_t r = fdiv(g, D.bpr);
         const uint32_t b = g - r * D.bpr.d;
-        in.a2 = D.a2[fmodu(r * D.groups + (b >> 2), D.n2)];
+        const uint8_t* pa1 = D.a1 + fmodu(g, D.nb);
+        const float* pa2 = D.a2 + fmodu(r * D.groups + (b >> 2), D.n2);
+        if constexpr (NF4_DQ_SCALE_NT) {
+            in.a1 = __builtin_nontemporal_load(pa1);
+            in.a2 = __builtin_nontemporal_load(pa2);
+        } else {
+            in.a1 = *pa1;
+            in.a2 = *pa2;
+        }
     } else if constexpr (MODE == kSingle) {
         const uint32_t r = fdiv(g, D.bpr);
         const uint32_t b = g - r * D.bpr.d;

@@ -134,7 +134,8 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
     if (c.kernel == NF4DQ_GEMM_SK) {
         // static rules only: whether the launch's column total spreads over the CUs is
         // checked at launch (sk_plan; a grouped launch counts every weight's columns)
-        return K % kSChunkK == 0 && M * K * 2 <= 65536 && c.waves == 8 && c.ksplit == 1;
+        return K % kSChunkK == 0 && M * K * 2 <= 65536 && c.waves == 8 && c.ksplit == 1 &&
+               (c.depth == 0 || c.depth == 2 || c.depth == 4 || c.depth == 8);
     }
     if (c.kernel == NF4DQ_GEMM_XS) {
         if (c.waves != 4 && c.waves != 8) return false;

@@ -17,6 +17,7 @@ int launch_sk(const HostMat* mats, int count, const void* x, int64_t M, int64_t 
     A.x = x;
     A.counters = reinterpret_cast<uint32_t*>(workspace);
     A.slab = p.slots > 1 ? reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(workspace) + kHeaderBytes) : nullptr;
+    A.xslab = A.slab ? A.slab + (size_t)p.slots * (size_t)M * (size_t)ncols / 2u : nullptr;
     A.M = (uint32_t)M;
     A.K = (uint32_t)K;
     A.C = make_fastdiv(p.C);
@@ -50,15 +51,21 @@ int launch_sk(const HostMat* mats, int count, const void* x, int64_t M, int64_t 
         strips += (uint32_t)(h.N / 16);
     }
     const dim3 grid(p.G), block(64 * p.W);
-#define NF4_SK1(DT_, LM_)                                                                                  \
+#define NF4_SK2(DT_, LM_, D_)                                                                              \
     do {                                                                                                   \
         static bool attr_ = false; /* static + dynamic LDS above 64 KiB needs the opt-in */                \
         if (!attr_) {                                                                                      \
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_sk_kernel<DT_, 8, LM_>),    \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&nf4_gemm_sk_kernel<DT_, 8, LM_, D_>),    \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSkLdsCap);         \
             attr_ = true;                                                                                  \
         }                                                                                                  \
-        hipLaunchKernelGGL((nf4_gemm_sk_kernel<DT_, 8, LM_>), grid, block, p.lds, st, A);                 \
+        hipLaunchKernelGGL((nf4_gemm_sk_kernel<DT_, 8, LM_, D_>), grid, block, p.lds, st, A);                 \
+    } while (0)
+#define NF4_SK1(DT_, LM_)                            \
+    do {                                             \
+        if (cfg.depth == 8) NF4_SK2(DT_, LM_, 8);    \
+        else if (cfg.depth == 2) NF4_SK2(DT_, LM_, 2); \
+        else NF4_SK2(DT_, LM_, 4);                   \
     } while (0)
 #define NF4_SKL(DT_)                          \
     do {                                      \
@@ -72,6 +79,7 @@ int launch_sk(const HostMat* mats, int count, const void* x, int64_t M, int64_t 
     else NF4_SKL(NF4DQ_F16);
 #undef NF4_SKL
 #undef NF4_SK1
+#undef NF4_SK2
     return hip_rc2(hipGetLastError());
 }
 

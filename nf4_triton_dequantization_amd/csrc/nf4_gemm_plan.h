@@ -186,7 +186,8 @@ inline bool sk_plan(int64_t M, int64_t K, int64_t ncols, int waves, SkPlan& p) {
 inline size_t sk_workspace(int64_t M, int64_t K, int64_t ncols, int waves) {
     SkPlan p{};
     if (!sk_plan(M, K, ncols, waves, p) || p.slots < 2) return 0;
-    return kHeaderBytes + (size_t)p.slots * (size_t)M * (size_t)ncols * 4u;  // 8-B entry per 2 columns
+    // the ticket slab [slots][M][ncols / 2], then the exchange entries [strip][M][8]: 8 B per 2 columns each
+    return kHeaderBytes + ((size_t)p.slots + 1u) * (size_t)M * (size_t)ncols * 4u;
 }
 
 }  // namespace

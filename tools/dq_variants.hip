@@ -10,6 +10,7 @@
 //   DQV_LD=p   cache-policy bits of the packed-weight loads (product 2 = nt; 16 = sc1, 1 = sc0, 0 = default)
 //   DQV_ST=p   cache-policy bits of the output stores (product 18 = sc1 + nt)
 //   DQV_SF=1   a tile's scale loads issued before its packed loads
+//   DQV_SNT=1  the absmax / nested-scale gathers with the nt policy
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
 #endif
@@ -24,6 +25,9 @@
 #endif
 #ifdef DQV_SF
 #define NF4_DQ_SCALE_FIRST DQV_SF
+#endif
+#ifdef DQV_SNT
+#define NF4_DQ_SCALE_NT DQV_SNT
 #endif
 
 #include "../nf4_triton_dequantization_amd/csrc/nf4_dequant.hip"

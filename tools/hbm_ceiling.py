@@ -1,6 +1,7 @@
 """What the memory system gives the dequant's access mix (speed-of-light check).
 
-Times, with hipGraph replay over rotating buffers (>> 256 MiB Infinity Cache):
+Times, with hipGraph replay over inputs and outputs rotated independently (>= 512
+MiB of distinct reads: the weights stream from HBM, profiles/r04/cache/):
   * calib_mix  -- nf4_flat_kernel's exact load/store shapes, no decode
                   (1 B read : 4 B written, like NF4 -> 16-bit)
   * calib_mix16 -- 16 B/lane loads (1 KiB per wave instruction), four strided 16 B
@@ -48,44 +49,38 @@ def main():
     C = ctypes.CDLL(os.path.join(REPO, "tools", "_build", "libpmccalib.so"))
     L = _lib.lib()
     for (m, n) in ((4096, 4096), (8192, 8192)):
-      for layout in ("separate", "interleaved"):
-        P = 16 if m == 4096 else 8
+        # round 4: inputs and outputs rotate independently, >= 512 MiB of distinct reads
+        # (the weights stream from HBM, as in bench.py) and >= 512 MiB of outputs
         nbytes = m * n // 2
         nb = m * n // 64
-        if layout == "separate":   # all inputs, then all outputs
-            ins = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=dev) for _ in range(P)]
-            outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(P)]
-        else:                      # input, output, input, output ... (what bench.py does)
-            ins, outs = [], []
-            for _ in range(P):
-                ins.append(torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=dev))
-                outs.append(torch.empty((m, n), dtype=torch.bfloat16, device=dev))
+        PI = -(-(512 << 20) // nbytes)
+        PO = -(-(512 << 20) // (4 * nbytes))
+        ins = [torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=dev) for _ in range(PI)]
+        outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(PO)]
         a1 = torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev)
         a2 = torch.rand((nb + 255) // 256, device=dev)
-        gaps = sorted({(outs[i].data_ptr() - ins[i].data_ptr()) % (1 << 21) for i in range(P)})
 
         def mix(i):
-            assert C.calib_mix_launch(ctypes.c_void_p(ins[i % P].data_ptr()), ctypes.c_uint32(nbytes),
-                                      ctypes.c_void_p(outs[i % P].data_ptr()),
+            assert C.calib_mix_launch(ctypes.c_void_p(ins[i % PI].data_ptr()), ctypes.c_uint32(nbytes),
+                                      ctypes.c_void_p(outs[i % PO].data_ptr()),
                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
 
         def mix16(i):
-            assert C.calib_mix16_launch(ctypes.c_void_p(ins[i % P].data_ptr()), ctypes.c_uint32(nbytes),
-                                        ctypes.c_void_p(outs[i % P].data_ptr()),
+            assert C.calib_mix16_launch(ctypes.c_void_p(ins[i % PI].data_ptr()), ctypes.c_uint32(nbytes),
+                                        ctypes.c_void_p(outs[i % PO].data_ptr()),
                                         ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
 
         def deq(i):
-            assert L.nf4_dequant_ref(ins[i % P].data_ptr(), nbytes, a1.data_ptr(), nb, a2.data_ptr(), a2.numel(),
-                                     outs[i % P].data_ptr(), _lib.BF16, m, n,
+            assert L.nf4_dequant_ref(ins[i % PI].data_ptr(), nbytes, a1.data_ptr(), nb, a2.data_ptr(), a2.numel(),
+                                     outs[i % PO].data_ptr(), _lib.BF16, m, n,
                                      torch.cuda.current_stream().cuda_stream) == 0
 
-        for name, fn, byt in (("calib_mix (same access shapes, no decode)", mix, nbytes * 5),
+        for name, fn, byt in (("calib_mix (same access shapes and policies, no decode)", mix, nbytes * 5),
                               ("calib_mix16 (16 B/lane loads, strided 16 B stores)", mix16, nbytes * 5),
                               ("nf4 dequant", deq, nbytes * 5 + nb + 4 * a2.numel())):
-            t = graph_time(fn, 64)
-            print(json.dumps({"kernel": name, "layout": layout, "m": m, "n": n, "us": t * 1e6,
-                              "GBps": byt / t / 1e9, "frac": byt / t / PEAK,
-                              "out_minus_in_mod_2MiB": gaps[:4]}), flush=True)
+            t = graph_time(fn, 2 * PI)
+            print(json.dumps({"kernel": name, "m": m, "n": n, "in_sets": PI, "out_sets": PO, "us": t * 1e6,
+                              "GBps": byt / t / 1e9, "frac": byt / t / PEAK}), flush=True)
         del ins, outs
         torch.cuda.empty_cache()
     buf = torch.empty(1 << 30, dtype=torch.uint8, device=dev)

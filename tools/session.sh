@@ -57,7 +57,7 @@ for stage in "$@"; do
         done ;;
     gstamps)  # fused-GEMM phase stamps (tools/_build/libnf4dq_gstamps.so, built here)
         for spec in ${GSTAMPS:-"14336,4096:32" "14336,4096:16" "14336,4096:1" "4096,4096:32" "4096,14336:32"}; do
-            timeout -k 10 200 $PY tools/gemm_stamps.py --shape ${spec%%:*} --m ${spec##*:} >> "$O/gemm_stamps.jsonl" 2>> "$O/gemm_stamps.err"
+            timeout -k 10 200 $PY tools/gemm_stamps.py --shape ${spec%%:*} --m ${spec##*:} ${GSTAMP_CFGS:-} >> "$O/gemm_stamps.jsonl" 2>> "$O/gemm_stamps.err"
         done
         cat "$O/gemm_stamps.jsonl" ;;
     dqab)  # interleaved dequant launch-config A/B: DQAB_ARGS passed to tools/dq_ab.py
@@ -80,6 +80,12 @@ for stage in "$@"; do
             NF4DQ_LIB_PATH=tools/_build/libnf4dq_$x.so timeout -k 10 300 $PY tools/gemm_ab.py ${GEMMAB_ARGS:-} >> "$O/gemm_ab.jsonl" 2>> "$O/gemm_ab.err"
         done
         cat "$O/gemm_ab.jsonl" ;;
+    gemmab2)  # a second decode-GEMM A/B with its own arguments (GEMMAB2_ARGS)
+        timeout -k 10 300 $PY tools/gemm_ab.py ${GEMMAB2_ARGS:-} >> "$O/gemm_ab2.jsonl" 2>> "$O/gemm_ab2.err"
+        cat "$O/gemm_ab2.jsonl" ;;
+    ceiling)  # memory-system twin of the dequant access mix vs the kernel (tools/hbm_ceiling.py)
+        timeout -k 10 300 $PY tools/hbm_ceiling.py > "$O/hbm_ceiling.jsonl" 2> "$O/hbm_ceiling.err"
+        cat "$O/hbm_ceiling.jsonl" ;;
     gemmtest)
         timeout -k 10 600 $PY -m pytest tests/test_gpu_gemm.py tests/test_gpu_redzones.py tests/test_gpu_concurrency.py -x -q \
             --timeout 300 --timeout-method thread > "$O/gemmtest.log" 2>&1 || { tail -30 "$O/gemmtest.log"; exit 1; }
