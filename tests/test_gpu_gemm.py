@@ -739,13 +739,13 @@ except ImportError:  # hypothesis is part of the test environment; keep the modu
     pass
 
 
-def _sk_call(L, _lib, x, mats, dt_code, K):
+def _sk_call(L, _lib, x, mats, dt_code, K, depth=0):
     """One NF4DQ_GEMM_SK launch over `mats` [(packed, a1, a2, y)] through the grouped
     ABI (one weight = a group of one); returns (rc, workspace)."""
     import ctypes
 
     M = x.shape[0]
-    cfg = _lib.GemmCfg(_lib.GEMM_SK, 8, 0, 1, 0)
+    cfg = _lib.GemmCfg(_lib.GEMM_SK, 8, depth, 1, 0)
     arr = (_lib.GemmMat * len(mats))()
     for i, (p, a1, a2, y) in enumerate(mats):
         arr[i] = _lib.GemmMat(p.data_ptr(), p.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
@@ -761,14 +761,16 @@ def _sk_call(L, _lib, x, mats, dt_code, K):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
-@pytest.mark.parametrize("M,Ns,K", [(1, (14336,), 4096), (4, (4096,), 4096), (8, (1024,), 4096), (1, (4096,), 14336),
-                                    (3, (4160,), 1280), (16, (2048,), 2048), (1, (4096, 1024, 1024), 4096),
-                                    (2, (14336, 14336), 4096), (5, (64, 4096, 192), 2048)])
-def test_balanced_kernel(coracle, gpu, dt, M, Ns, K):
+@pytest.mark.parametrize("M,Ns,K,depth", [(1, (14336,), 4096, 0), (4, (4096,), 4096, 2), (8, (1024,), 4096, 8),
+                                          (1, (4096,), 14336, 0), (3, (4160,), 1280, 4), (16, (2048,), 2048, 2),
+                                          (1, (4096, 1024, 1024), 4096, 8), (2, (14336, 14336), 4096, 2),
+                                          (5, (64, 4096, 192), 2048, 0), (1, (28672,), 4096, 8)])
+def test_balanced_kernel(coracle, gpu, dt, M, Ns, K, depth):
     """NF4DQ_GEMM_SK: equal (strip, 256-deep chunk) ranges per wave, strips shared by
     workgroups summed through the slab (the 1024-column weight: four workgroups per
     strip; 4160 x 1280: ragged strip count, 5 chunks per strip; down projection: 56;
-    grouped launches with a 64-column weight inside a group).  Checked against the
+    grouped launches with a 64-column weight inside a group; 28672 columns: 16 units per
+    wave through an 8-deep ring), every ring depth.  Checked against the
     float64 oracle of the reference's weights, the workspace back at zero with no
     split-K error, and a second launch bitwise identical (fixed summation order)."""
     from nf4_triton_dequantization_amd import _lib
@@ -783,7 +785,7 @@ def test_balanced_kernel(coracle, gpu, dt, M, Ns, K):
         Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16))
         mats.append((torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu),
                      torch.full((M, N), float("nan"), dtype=x.dtype, device=gpu)))
-    rc, chk, ws, wsz = _sk_call(L, _lib, x, mats, code, K)
+    rc, chk, ws, wsz = _sk_call(L, _lib, x, mats, code, K, depth)
     assert rc == 0, _lib.strerror(rc)
     assert chk == 0, _lib.strerror(chk)
     if wsz:
@@ -792,7 +794,7 @@ def test_balanced_kernel(coracle, gpu, dt, M, Ns, K):
     for (_, _, _, y), W in zip(mats, Ws):
         assert not bool(torch.isnan(y).any())
         _check(y, xb, W, dt)
-    rc, chk, _, _ = _sk_call(L, _lib, x, mats, code, K)
+    rc, chk, _, _ = _sk_call(L, _lib, x, mats, code, K, depth)
     assert rc == 0 and chk == 0
     for y0, m in zip(first, mats):
         assert torch.equal(y0.view(torch.int16), m[3].view(torch.int16)), "not bitwise reproducible"
