@@ -100,6 +100,12 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 #ifndef NF4_ABL_RING_FULL
 #define NF4_ABL_RING_FULL 1
 #endif
+#ifndef NF4_ABL_ENTRY_RETURN  // tools: persistent kernel returns at entry (launch cost alone)
+#define NF4_ABL_ENTRY_RETURN 0
+#endif
+#ifndef NF4_ABL_LOOP_ON  // tools: persistent kernel skips its chunk loop (prologue + epilogue alone)
+#define NF4_ABL_LOOP_ON 1
+#endif
 #ifndef NF4_ABL_KEEP_SLICE
 #define NF4_ABL_KEEP_SLICE(ks_) true
 #endif
@@ -1599,6 +1605,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t nl = lane & 15u, kh = lane >> 4;
     const uint32_t strip_in = wave % A.T, part = wave / A.T;
+    if constexpr (NF4_ABL_ENTRY_RETURN) return;
     // K slices: workgroup b works on slice b % ksplit (its x slice staged once),
     // walking the strip groups b / ksplit, + G / ksplit, ...
     const uint32_t KS = SPLIT ? A.ksplit : 1u, ks = SPLIT ? blockIdx.x % KS : 0u;
@@ -1738,7 +1745,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
             ++it;
         }
     };
-    for (uint32_t g = 0; g < total; g += 2) {
+    for (uint32_t g = 0; g < (NF4_ABL_LOOP_ON ? total : 0u); g += 2) {
         round(sc[0], sc[1]);
         if (g + 1 < total) round(sc[1], sc[0]);
     }

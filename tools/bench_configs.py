@@ -7,11 +7,12 @@ c3   Llama-3-8B: 32 layers x {q,o 4096x4096; k,v 1024x4096; gate,up 14336x4096;
      C ABI (nf4_dequant_ref_batched, <= NF4DQ_BATCH_MAX matrices per launch).
 c3b  the "4096/11008" shape set BASELINE names (Llama-2-7B: q,k,v,o 4096x4096;
      gate,up 11008x4096; down 4096x11008), same method.
-c4   4096x4096 NF4 -> fp16 vs bf16 vs fp32 output, single launches over rotating
-     buffer sets (13 for 16-bit output, as bench.py: >= 512 MiB), timed as bench.py times its steps
+c4   4096x4096 NF4 -> fp16 vs bf16 vs fp32 output, single launches over an
+     independent input / output rotation (>= 512 MiB of distinct reads and of distinct
+     writes, bench.py's HBM-streamed regime), timed as bench.py times its steps
      (eager, behind a device spin), the hipGraph replay beside it.
-c5   one 8192x8192 NF4->bf16 matrix (the per-GPU unit of the 8-GPU config), 4 sets,
-     the same method.
+c5   one 8192x8192 NF4->bf16 matrix (the per-GPU unit of the 8-GPU config), the same
+     rotation and method.
 big  128256x8192 NF4->bf16 (Llama-3-70B lm_head size: 525 MB packed, past one buffer
      descriptor -- two row pieces in one launch).
 bnb  4096x4096 NF4->bf16 with bitsandbytes semantics (nf4_dequant_bnb: code2[A1] * A2
@@ -158,23 +159,57 @@ def eager_per_launch(launch, steps, reps):
     return ts[len(ts) // 2]
 
 
-def run_single(name, m, n, dt, code, reps, dev, sets=16, steps=64):
-    """Single launches over `sets` rotating buffer sets.  Timed as bench.py times its
-    steps (eager launches behind a spin, ``us_per_launch``); the hipGraph replay of
-    the same launches is reported beside it (``graph_us_per_launch``): on ROCm 7.2 a
-    replay adds 1-3 us per 8192^2 kernel, as a system-scope release between eager
-    launches does (tools/c5_probe.py, profiles/r03/c5/)."""
+MIN_READ_FOOTPRINT = 512 << 20  # bench.py's HBM-streamed rotation (DESIGN.md "cache regime")
+MIN_WRITE_FOOTPRINT = 512 << 20
+
+
+def rotation(m, n, ob, extra_read=0):
+    """(input sets, output sets): >= 512 MiB of distinct reads and of distinct writes,
+    as bench.rotation_sets -- every launch reads its packed weight from HBM."""
+    rd = m * n // 2 + m * n // 64 + 4 * ((m * n // 64 + 255) // 256) + extra_read
+    wr = m * n * ob
+    return max(1, -(-MIN_READ_FOOTPRINT // rd)), max(1, -(-MIN_WRITE_FOOTPRINT // wr))
+
+
+def rotating_sets(m, n, dt, dev, gen, pin, pout):
+    """pin (packed, absmax, absmax2) input sets and pout output buffers."""
+    ins = [make_weight(m, n, dev, gen, dt)[:3] for _ in range(pin)]
+    outs = [torch.empty((m, n), dtype=dt, device=dev) for _ in range(pout)]
+    return ins, outs
+
+
+def last_writes(pin, pout, steps, limit=4):
+    """(input set, output set) of the last timed launch that wrote each of the first
+    `limit` output sets: what the outputs hold when the timing ends."""
+    res = []
+    for j in range(min(pout, steps, limit)):
+        i = j + ((steps - 1 - j) // pout) * pout
+        res.append((i % pin, j))
+    return res
+
+
+def run_single(name, m, n, dt, code, reps, dev, steps=64):
+    """Single launches over an independent input / output rotation (step i reads input
+    set i % Pin, writes output set i % Pout; >= 512 MiB distinct reads and writes, the
+    regime of bench.py's headline).  Timed as bench.py times its steps (eager launches
+    behind a spin, ``us_per_launch``); the hipGraph replay of the same launches is
+    reported beside it (``graph_us_per_launch``): on ROCm 7.2 a replay adds 1-3 us per
+    8192^2 kernel, as a system-scope release between eager launches does
+    (tools/c5_probe.py, profiles/r03/c5/)."""
     gen = torch.Generator(device=dev)
     gen.manual_seed(1)
-    ws = [make_weight(m, n, dev, gen, dt) for _ in range(sets)]
+    ob = torch.empty((), dtype=dt).element_size()
+    pin, pout = rotation(m, n, ob)
+    ins, outs = rotating_sets(m, n, dt, dev, gen, pin, pout)
     L = _lib.lib()
 
     def launch(i):
-        q, a1, a2, o = ws[i % sets]
+        q, a1, a2 = ins[i % pin]
+        o = outs[i % pout]
         assert L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
                                  o.data_ptr(), code, m, n, torch.cuda.current_stream().cuda_stream) == 0
 
-    for i in range(sets):  # every set touched once (TLB-warm, as resident weights are)
+    for i in range(max(pin, pout)):  # every set touched once (TLB-warm, as resident weights are)
         launch(i)
     torch.cuda.synchronize()
     t = eager_per_launch(launch, steps, reps)
@@ -183,21 +218,23 @@ def run_single(name, m, n, dt, code, reps, dev, sets=16, steps=64):
         for i in range(steps):
             launch(i)
     tg = timed(graph.replay, reps) / steps
-    ob = torch.empty((), dtype=dt).element_size()
     byt = alg_bytes(m, n, ob)
-    checked = verify(ws[:min(sets, steps)], code)
-    fp = sets * (m * n // 2 + m * n * ob + m * n // 64)
+    checked = verify([ins[a] + (outs[b],) for a, b in last_writes(pin, pout, steps)], code)
+    rd = pin * (m * n // 2 + m * n // 64 + 4 * ((m * n // 64 + 255) // 256))
     return {"config": name, "verified": True, "verified_matrices": checked, "m": m, "n": n,
-            "out_dtype": str(dt).replace("torch.", ""), "sets": sets, "footprint_bytes": fp,
+            "out_dtype": str(dt).replace("torch.", ""), "in_sets": pin, "out_sets": pout,
+            "read_footprint_bytes": rd, "write_footprint_bytes": pout * m * n * ob,
+            "weights_from": "HBM (distinct reads >= 512 MiB)" if rd >= MIN_READ_FOOTPRINT else "Infinity Cache possible",
             "us_per_launch": t * 1e6, "elements_per_s": m * n / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9,
             "frac": byt / t / PEAK, "timing": "eager launches behind a spin (bench.py's method)",
             "graph_us_per_launch": tg * 1e6, "graph_frac": byt / tg / PEAK}
 
 
-def run_bnb(name, m, n, reps, dev, sets=16, steps=64):
+def run_bnb(name, m, n, reps, dev, steps=64):
     gen = torch.Generator(device=dev)
     gen.manual_seed(2)
-    ws = [make_weight(m, n, dev, gen, torch.bfloat16) for _ in range(sets)]
+    pin, pout = rotation(m, n, 2)
+    ins, outs = rotating_sets(m, n, torch.bfloat16, dev, gen, pin, pout)
     code2 = torch.linspace(-1, 1, 256, device=dev, dtype=torch.float32)
     L = _lib.lib()
     numel = m * n
@@ -205,16 +242,19 @@ def run_bnb(name, m, n, reps, dev, sets=16, steps=64):
     with torch.cuda.graph(graph):
         sp = torch.cuda.current_stream().cuda_stream
         for i in range(steps):
-            q, a1, a2, o = ws[i % sets]
+            q, a1, a2 = ins[i % pin]
             assert L.nf4_dequant_bnb(q.data_ptr(), a1.data_ptr(), a1.numel(), code2.data_ptr(), a2.data_ptr(),
-                                     a2.numel(), ctypes.c_float(0.0123), o.data_ptr(), _lib.BF16, numel, 64, 256,
-                                     sp) == 0
+                                     a2.numel(), ctypes.c_float(0.0123), outs[i % pout].data_ptr(), _lib.BF16, numel,
+                                     64, 256, sp) == 0
     t = timed(graph.replay, reps) / steps
     nb = numel // 64
     byt = numel // 2 + 2 * numel + nb + 4 * ((nb + 255) // 256) + 1024
-    checked = verify(ws[:min(sets, steps)], _lib.BF16, bnb_code2=code2.cpu().numpy(), bnb_offset=np.float32(0.0123))
-    return {"config": name, "verified": True, "verified_matrices": checked, "m": m, "n": n, "out_dtype": "bfloat16", "us_per_launch": t * 1e6,
-            "elements_per_s": numel / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK}
+    checked = verify([ins[a] + (outs[b],) for a, b in last_writes(pin, pout, steps)], _lib.BF16,
+                     bnb_code2=code2.cpu().numpy(), bnb_offset=np.float32(0.0123))
+    return {"config": name, "verified": True, "verified_matrices": checked, "m": m, "n": n, "out_dtype": "bfloat16",
+            "in_sets": pin, "out_sets": pout, "us_per_launch": t * 1e6,
+            "elements_per_s": numel / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK,
+            "timing": "hipGraph replay of the launches"}
 
 
 def main():
@@ -235,18 +275,16 @@ def main():
         torch.cuda.empty_cache()
     if "c4" in todo:
         for dt, code in ((torch.float16, _lib.F16), (torch.bfloat16, _lib.BF16), (torch.float32, _lib.F32)):
-            print(json.dumps(run_single("c4 4096x4096 dtype sweep", 4096, 4096, dt, code, args.reps, dev,
-                                        sets=13 if dt != torch.float32 else 8)), flush=True)
+            print(json.dumps(run_single("c4 4096x4096 dtype sweep", 4096, 4096, dt, code, args.reps, dev)),
+                  flush=True)
+        torch.cuda.empty_cache()
     if "c5" in todo:
-        # 4 sets = 675 MB: the flat HBM regime of bench.py's MIN_FOOTPRINT (past the
-        # Infinity Cache, short of the ~1.2 GB footprint where every launch pays ~10 %)
-        print(json.dumps(run_single("c5 8192x8192 per-GPU unit", 8192, 8192, torch.bfloat16, _lib.BF16, args.reps, dev,
-                                    sets=4, steps=64)), flush=True)
-
-
+        print(json.dumps(run_single("c5 8192x8192 per-GPU unit", 8192, 8192, torch.bfloat16, _lib.BF16, args.reps, dev)),
+              flush=True)
+        torch.cuda.empty_cache()
     if "big" in todo:
         print(json.dumps(run_single("big 128256x8192 (a 70B lm_head: two flat pieces, one launch)", 128256, 8192,
-                                    torch.bfloat16, _lib.BF16, args.reps, dev, sets=2, steps=8)), flush=True)
+                                    torch.bfloat16, _lib.BF16, args.reps, dev, steps=8)), flush=True)
         torch.cuda.empty_cache()
     if "bnb" in todo:
         print(json.dumps(run_bnb("bnb-semantics 4096x4096 NF4->bf16", 4096, 4096, args.reps, dev)), flush=True)

@@ -12,6 +12,8 @@
 //   ABL_NOSCALE register-resident kernel: no absmax byte / nested scale gathers
 //   ABL_NORING  ABL_NOWLOAD + ABL_NOSCALE: the ring issues no memory operation
 //   ABL_L2WIN   weight loads folded into a 256 KiB window (L2-resident, same instructions)
+//   ABL_EMPTY   persistent kernel: returns at entry (the launch of its grid, nothing else)
+//   ABL_NOLOOP  persistent kernel: no chunk loop (x staging, tables, outputs: the fixed cost)
 //   ABL_NTW     weight loads with the nt policy (a variant, not an ablation: correct results)
 //   ABL_DROPSLICE  128-deep kernel: K slice 1 withholds its split-K partials (takes its
 //               ticket all the same), so the reducer's bounded poll gives up: proves the
@@ -20,6 +22,12 @@
 
 #if defined(ABL_NTW)  // weight loads with the nt (streaming) policy, as the flat dequant kernel's
 #define NF4_ABL_WLOAD(rsrc_, off_) __builtin_amdgcn_raw_buffer_load_b128((rsrc_), (off_), 0, 2)
+#endif
+#if defined(ABL_EMPTY)
+#define NF4_ABL_ENTRY_RETURN 1
+#endif
+#if defined(ABL_NOLOOP)
+#define NF4_ABL_LOOP_ON 0
 #endif
 #if defined(ABL_DROPSLICE)
 #define NF4_ABL_KEEP_SLICE(ks_) ((ks_) != 1u)
