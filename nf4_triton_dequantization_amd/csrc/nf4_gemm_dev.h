@@ -103,6 +103,12 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 #ifndef NF4_ABL_ENTRY_RETURN  // tools: persistent kernel returns at entry (launch cost alone)
 #define NF4_ABL_ENTRY_RETURN 0
 #endif
+#ifndef NF4_ABL_PLOAD_FAKE  // tools: persistent kernel's scale loads made from their offsets
+#define NF4_ABL_PLOAD_FAKE 0
+#endif
+#ifndef NF4_PERSIST_PAIR  // persistent kernel: two ring slots decoded step-interleaved (even P)
+#define NF4_PERSIST_PAIR 0
+#endif
 #ifndef NF4_ABL_LOOP_ON  // tools: persistent kernel skips its chunk loop (prologue + epilogue alone)
 #define NF4_ABL_LOOP_ON 1
 #endif
@@ -1382,6 +1388,59 @@ __device__ __forceinline__ void sslot_mma(const SSlot& s, uint32_t qa, float qb,
     }
 }
 
+// Two chunks of one strip (one row tile, M <= 16) decoded step by step side by
+// side: two independent chains of pair lookups, x reads and MFMAs, so that one
+// chunk's LDS round trips overlap the other's VALU work.  Scales come in computed.
+template <int DT>
+__device__ __forceinline__ void sslot_mma_pair(const SSlot& s0, const SSlot& s1, float scA, float scB,
+                                               const f32x2* ptab, const char* smem, uint32_t slot8, uint32_t xaA,
+                                               uint32_t xaB, f32x4& acc, f32x4& accb) {
+    const f32x2 sA = {scA, opaque(scA)}, sB = {scB, opaque(scB)};
+    const char* pt = reinterpret_cast<const char*>(ptab);
+    constexpr int LA = 2;
+    f32x2 vA[8][4], vB[8][4];
+    auto issue = [&](int st) {
+        const uint32_t wa = st < 4 ? s0.w0[st] : s0.w1[st - 4];
+        const uint32_t wb = st < 4 ? s1.w0[st] : s1.w1[st - 4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t sel = 0x0C0C0000u | ((4u + b) << 8);
+            vA[st][b] = NF4_ABL_LOOKUP(pt, __builtin_amdgcn_perm(wa, slot8, sel), wa);
+            vB[st][b] = NF4_ABL_LOOKUP(pt, __builtin_amdgcn_perm(wb, slot8, sel), wb);
+        }
+    };
+#pragma unroll
+    for (int st = 0; st < LA; ++st) issue(st);
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+        if (st + LA < 8) issue(st + LA);
+        const u32x4 a0 = *reinterpret_cast<const u32x4*>(smem + xaA + 16u * st);
+        const u32x4 a1 = *reinterpret_cast<const u32x4*>(smem + xaB + 16u * st);
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t bw0[4], bw1[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const f32x2 p0 = vA[st][b] * sA, p1 = vB[st][b] * sB;  // fp32 products (:97-98)
+            bw0[b] = pack2<DT>(p0.x, p0.y);                          // RNE (:109-110)
+            bw1[b] = pack2<DT>(p1.x, p1.y);
+        }
+        const u32x4 bq0 = {bw0[0], bw0[1], bw0[2], bw0[3]}, bq1 = {bw1[0], bw1[1], bw1[2], bw1[3]};
+        if constexpr (!NF4_ABL_MMA_ON) {
+            asm volatile("" ::"v"(a0), "v"(a1), "v"(bq0), "v"(bq1));
+        } else if constexpr (DT == NF4DQ_BF16) {
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0), __builtin_bit_cast(bf16x8, bq0),
+                                                          acc, 0, 0, 0);
+            accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1),
+                                                           __builtin_bit_cast(bf16x8, bq1), accb, 0, 0, 0);
+        } else {
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a0), __builtin_bit_cast(f16x8, bq0),
+                                                         acc, 0, 0, 0);
+            accb = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a1), __builtin_bit_cast(f16x8, bq1),
+                                                          accb, 0, 0, 0);
+        }
+    }
+}
+
 // VS: vector scales -- no absmax wrap inside a row (nb a multiple of K / 64 or
 // >= N K / 64, n2 a multiple of groups or >= N groups: true for every real
 // bitsandbytes state, where n2 = N groups / 64) and at most kVsMax chunks per wave: the wave's absmax bytes (4 per chunk) and nested
@@ -1587,13 +1646,19 @@ struct PScales {
 
 template <int P>
 __device__ __forceinline__ typename PScales<P>::vec pload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    if constexpr (P == 2) return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    if constexpr (NF4_ABL_PLOAD_FAKE) {  // tools: scales made from the offset (no gather)
+        typename PScales<P>::vec v;
+#pragma unroll
+        for (int i = 0; i < P; ++i) v[i] = 0x3C000000u | ((off * 37u + (uint32_t)i) & 0x7F7Fu);
+        return v;
+    } else if constexpr (P == 2) return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
     else return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 
 struct PGeo {  // where the ring issues: one strip of one weight
     __amdgpu_buffer_rsrc_t rw, ra1, ra2;
     uint32_t row, b1, b2;
+    uint32_t wbase;  // the lane's first weight byte of the slice: row K / 2 + kh 32 + chunk base 128
 };
 
 template <int DT, int W, int P, bool SPLIT>
@@ -1629,6 +1694,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         g.ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a2, 0, Mt.n2_bytes, kRsrcFlags);
         g.b1 = fmodu(g.row * A.bpr, Mt.nb) + 4u * (cbase + l0);  // reference wrap (:173-186), none inside a row
         g.b2 = fmodu(g.row * A.groups, Mt.n2) + cbase + l0;
+        g.wbase = g.row * (A.K >> 1) + (cbase + l0) * 128u + kh * 32u;
     };
     // issue pointer: group it2, round rr2 of it
     PGeo gi;
@@ -1640,8 +1706,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         sc.a2 = pload<P>(gi.ra2, ((gi.b2 + P * rr2) * 4u) | oob);
     };
     auto issue_w = [&](SSlot& sl, int s, bool valid) {
-        const uint32_t c = cbase + l0 + rr2 * P + (uint32_t)s;
-        const uint32_t woff = (gi.row * (A.K >> 1) + c * 128u + kh * 32u) | (valid ? 0u : kOob);
+        const uint32_t woff = (gi.wbase + (rr2 * P + (uint32_t)s) * 128u) | (valid ? 0u : kOob);
         sl.w0 = NF4_ABL_WLOAD(gi.rw, woff);
         sl.w1 = NF4_ABL_WLOAD(gi.rw, woff + 16u);
     };
@@ -1701,6 +1766,22 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
         const bool more = it2 < mine;  // the issue pointer is one round ahead
         issue_scales(nxt, more);
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (NF4_PERSIST_PAIR && P % 2 == 0) {
+#pragma unroll
+            for (int s = 0; s < P; s += 2) {
+                const uint32_t l = l0 + rr * P + (uint32_t)s;
+                const uint32_t xa = live ? xa0 + l * 512u : xa0, xb = live ? xa + 512u : xa0;
+                const float scA = qtab[(cur.a1[s] >> (8u * kh)) & 0xFFu] * __uint_as_float(cur.a2[s]);  // (:45, :97-98)
+                const float scB = qtab[(cur.a1[s + 1] >> (8u * kh)) & 0xFFu] * __uint_as_float(cur.a2[s + 1]);
+                sslot_mma_pair<DT>(ring[s], ring[s + 1], scA, scB, ptab, smem, slot8, xa, xb, acc[0], accb[0]);
+                if (it == 0 && rr == 0 && s == 0) NF4_GSTAMP(2);
+                __builtin_amdgcn_sched_barrier(0);
+                issue_w(ring[s], s, more);
+                __builtin_amdgcn_sched_barrier(0);
+                issue_w(ring[s + 1], s + 1, more);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
 #pragma unroll
         for (int s = 0; s < P; ++s) {
             const uint32_t l = l0 + rr * P + (uint32_t)s;
@@ -1711,6 +1792,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
             __builtin_amdgcn_sched_barrier(0);
             issue_w(ring[s], s, more);
             __builtin_amdgcn_sched_barrier(0);
+        }
         }
         advance();
         if (++rr == rounds) {  // group `it` done (uniform)
@@ -1755,16 +1837,21 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     NF4_GSTAMP(4);
     const uint32_t per = A.T * A.M * 16u;
     if constexpr (!SPLIT) {
+        // one held strip per wave at a time: wave w stores strips w, w + W, ... of the
+        // workgroup's (group, strip) list, [M][16] values 64 per pass (T is 1, 2 or 4:
+        // no divisions; the weight is a uniform scan)
         const uint16_t* o = reinterpret_cast<const uint16_t*>(smem + A.out_off);
-        for (uint32_t i = tid; i < mine * per; i += 64u * W) {
-            const uint32_t ito = i / per, rem = i - ito * per;
-            const uint32_t t = rem / (A.M * 16u), rem2 = rem - t * (A.M * 16u);
+        const uint32_t tsh = A.T == 4u ? 2u : A.T == 2u ? 1u : 0u;
+        for (uint32_t q = wave; q < (mine << tsh); q += W) {
+            const uint32_t ito = q >> tsh, t = q & (A.T - 1u);
             const uint32_t sgi = j0 + ito * G;
             uint32_t mi = 0;
             for (uint32_t j = 1; j < A.nmat; ++j) mi = sgi >= A.mat[j].sg_begin ? j : mi;
             const StreamMat& Mt = A.mat[mi];
-            const uint32_t col = ((sgi - Mt.sg_begin) * A.T + t) * 16u + (rem2 & 15u);
-            reinterpret_cast<uint16_t*>(Mt.y)[(rem2 >> 4) * Mt.N + col] = o[i];
+            const uint32_t col0 = ((sgi - Mt.sg_begin) * A.T + t) * 16u;
+            const uint16_t* os = o + q * A.M * 16u;  // (ito T + t) M 16
+            for (uint32_t e = lane; e < A.M * 16u; e += 64u)
+                reinterpret_cast<uint16_t*>(Mt.y)[(e >> 4) * Mt.N + col0 + (e & 15u)] = os[e];
         }
         NF4_GSTAMP(5);
     } else {

@@ -238,15 +238,19 @@ def run_bnb(name, m, n, reps, dev, steps=64):
     code2 = torch.linspace(-1, 1, 256, device=dev, dtype=torch.float32)
     L = _lib.lib()
     numel = m * n
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        sp = torch.cuda.current_stream().cuda_stream
-        for i in range(steps):
-            q, a1, a2 = ins[i % pin]
-            assert L.nf4_dequant_bnb(q.data_ptr(), a1.data_ptr(), a1.numel(), code2.data_ptr(), a2.data_ptr(),
-                                     a2.numel(), ctypes.c_float(0.0123), outs[i % pout].data_ptr(), _lib.BF16, numel,
-                                     64, 256, sp) == 0
-    t = timed(graph.replay, reps) / steps
+
+    def launch(i):
+        q, a1, a2 = ins[i % pin]
+        assert L.nf4_dequant_bnb(q.data_ptr(), a1.data_ptr(), a1.numel(), code2.data_ptr(), a2.data_ptr(),
+                                 a2.numel(), ctypes.c_float(0.0123), outs[i % pout].data_ptr(), _lib.BF16, numel,
+                                 64, 256, torch.cuda.current_stream().cuda_stream) == 0
+
+    for i in range(max(pin, pout)):
+        launch(i)
+    torch.cuda.synchronize()
+    t = eager_per_launch(launch, steps, reps)
+    for i in range(steps):  # the outputs the checker reads: the same launches in order
+        launch(i)
     nb = numel // 64
     byt = numel // 2 + 2 * numel + nb + 4 * ((nb + 255) // 256) + 1024
     checked = verify([ins[a] + (outs[b],) for a, b in last_writes(pin, pout, steps)], _lib.BF16,
@@ -254,7 +258,7 @@ def run_bnb(name, m, n, reps, dev, steps=64):
     return {"config": name, "verified": True, "verified_matrices": checked, "m": m, "n": n, "out_dtype": "bfloat16",
             "in_sets": pin, "out_sets": pout, "us_per_launch": t * 1e6,
             "elements_per_s": numel / t, "algorithmic_bytes": byt, "GBps": byt / t / 1e9, "frac": byt / t / PEAK,
-            "timing": "hipGraph replay of the launches"}
+            "timing": "eager launches behind a spin (bench.py's method)"}
 
 
 def main():

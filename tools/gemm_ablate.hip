@@ -12,6 +12,8 @@
 //   ABL_NOSCALE register-resident kernel: no absmax byte / nested scale gathers
 //   ABL_NORING  ABL_NOWLOAD + ABL_NOSCALE: the ring issues no memory operation
 //   ABL_L2WIN   weight loads folded into a 256 KiB window (L2-resident, same instructions)
+//   ABL_SKELETON ABL_NORING + ABL_NOLUT + ABL_NOMMA: control flow, x staging, tables, VALU
+//   ABL_PAIR    persistent kernel: two ring slots decoded step-interleaved (variant: correct results)
 //   ABL_EMPTY   persistent kernel: returns at entry (the launch of its grid, nothing else)
 //   ABL_NOLOOP  persistent kernel: no chunk loop (x staging, tables, outputs: the fixed cost)
 //   ABL_NTW     weight loads with the nt policy (a variant, not an ablation: correct results)
@@ -23,6 +25,9 @@
 #if defined(ABL_NTW)  // weight loads with the nt (streaming) policy, as the flat dequant kernel's
 #define NF4_ABL_WLOAD(rsrc_, off_) __builtin_amdgcn_raw_buffer_load_b128((rsrc_), (off_), 0, 2)
 #endif
+#if defined(ABL_PAIR)  // a variant, not an ablation: correct results
+#define NF4_PERSIST_PAIR 1
+#endif
 #if defined(ABL_EMPTY)
 #define NF4_ABL_ENTRY_RETURN 1
 #endif
@@ -33,6 +38,11 @@
 #define NF4_ABL_KEEP_SLICE(ks_) ((ks_) != 1u)
 #endif
 
+#if defined(ABL_SKELETON)  // the ring's memory operations, the lookups and the MFMAs all removed
+#define ABL_NORING
+#define ABL_NOLUT
+#define ABL_NOMMA
+#endif
 #if defined(ABL_NORING)  // no memory traffic in the ring at all
 #define ABL_NOWLOAD
 #define ABL_NOSCALE
@@ -48,6 +58,9 @@
 #define NF4_ABL_WLOAD(rsrc_, off_) (u32x4{(off_), (off_) * 3u, (off_) ^ 0x5A5A5A5Au, (off_) + 0x01010101u})
 #elif defined(ABL_L2WIN)  // weight loads folded into a 256 KiB window per weight: L2 hits, same instructions
 #define NF4_ABL_WLOAD(rsrc_, off_) __builtin_amdgcn_raw_buffer_load_b128((rsrc_), (off_) & 0x8003FFF0u, 0, 0)
+#endif
+#if defined(ABL_NOSCALE)  // (the persistent kernel's 8/16-byte scale loads too)
+#define NF4_ABL_PLOAD_FAKE 1
 #endif
 #if defined(ABL_NOSCALE)  // absmax byte / nested scale from the offset (no gather)
 #define NF4_ABL_SLOAD(rsrc_, off_, b8_) ((b8_) ? (((off_) * 37u) & 0x7Fu) | 1u : 0x3C000000u | ((off_) & 0xFFFFu))

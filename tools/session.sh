@@ -118,6 +118,20 @@ for stage in "$@"; do
             --output-format csv -d "$O/pmcg_b" -o b -- python3 -u $GA > "$O/pmcg_b.log" 2>&1
         python3 tools/pmc_gemm.py "$O" nf4_gemm_xrg_kernel nf4_gemm_xr_kernel nf4_gemm_persist_kernel nf4_gemm_stream_kernel > "$O/pmc_gemm.jsonl"
         cat "$O/pmc_gemm.jsonl" ;;
+    pmcg)  # decode-GEMM SQ counters only (PMC_M, PMC_SHAPE; NF4DQ_LIB_PATH selects a build)
+        GA="tools/gemm_ab.py --ms ${PMC_M:-1} --shapes ${PMC_SHAPE:-14336,4096} --budget-mb 512"
+        timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM --output-format csv -d "$O/pmcg_a" -o a -- \
+            python3 -u $GA > "$O/pmcg_a.log" 2>&1
+        timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INST_LEVEL_VMEM \
+            SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_VMEM_TA_ADDR_FIFO_FULL \
+            --output-format csv -d "$O/pmcg_b" -o b -- python3 -u $GA > "$O/pmcg_b.log" 2>&1
+        timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA \
+            SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY \
+            --output-format csv -d "$O/pmcg_c" -o c -- python3 -u $GA > "$O/pmcg_c.log" 2>&1
+        python3 tools/pmc_gemm.py "$O" nf4_gemm_persist_kernel nf4_gemm_xrg_kernel nf4_gemm_xr_kernel > "$O/pmcg${PMC_TAG:-}.jsonl"
+        rm -rf "$O/pmcg_a" "$O/pmcg_b" "$O/pmcg_c"
+        cat "$O/pmcg${PMC_TAG:-}.jsonl" ;;
     sweep)  # fused-GEMM decomposition sweep: SWEEP_ARGS passed to tools/sweep_gemm.py
         timeout -k 10 600 $PY tools/sweep_gemm.py ${SWEEP_ARGS:-} > "$O/sweep_gemm.jsonl" 2> "$O/sweep_gemm.err"
         python3 -c "import json,sys
