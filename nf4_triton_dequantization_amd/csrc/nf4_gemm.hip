@@ -59,6 +59,12 @@ static nf4_gemm_cfg nonpersist_cfg(int64_t M, int64_t N, int64_t K) {
         // chunks: per launch at M = 32 (profiles/r02/sweep_gemm_xr.jsonl) 20.4 vs 21.7 us
         // on 14336x4096, 11.9 vs 12.3 on 4096^2, 23.5 vs 24.6 on 4096x14336, 13.8 vs 14.2
         // on grouped q/k/v (6144), 31.4 vs 37.2 on grouped gate/up (28672)
+        if (M <= 24 && N >= 24576) {
+            // the widest launches (grouped gate/up) at M <= 24: 16 waves span K = 4096,
+            // no split-K hand-off: 26.0 vs 27.6 us (profiles/r04/gemm/xr_no_handoff_m24_m32.jsonl)
+            const nf4_gemm_cfg w{NF4DQ_GEMM_XR, 16, 2, (int)((K / kChunkK + 31) / 32), 2};
+            if (valid_gemm_cfg(w, M, N, K)) return w;
+        }
         const nf4_gemm_cfg c{NF4DQ_GEMM_XR, 8, 2, (int)((K / kChunkK + 15) / 16), 2};
         if (valid_gemm_cfg(c, M, N, K)) return c;
     }
