@@ -99,6 +99,7 @@ ROUNDS = ("r04", "r03", "r02", "r01")  # profiles/<round>/pmc_traffic.json, newe
 MIN_READ_FOOTPRINT = 512 << 20
 MIN_WRITE_FOOTPRINT = 512 << 20
 CACHE_WARM_SETS = 13
+C5_MIN_STEPS = 100  # the c5 object's timed steps at least (its launches are 27-215 us)
 
 
 def log(*a):
@@ -123,6 +124,9 @@ def parse_args(argv=None):
     ap.add_argument("--launch", default="eager", choices=["eager", "graph"],
                     help="timed steps as eager C-ABI launches (default) or one hipGraph replay")
     ap.add_argument("--no-graph", action="store_true", help="same as --launch eager (kept for old scripts)")
+    ap.add_argument("--spin-us-per-launch", type=float, default=30.0,
+                    help="--lead spin-steps: device spin per launch to be submitted (us); profilers that "
+                         "intercept every dispatch need more (tools/session.sh rocprof uses 150)")
     ap.add_argument("--lead", default="auto", choices=["auto", "replay", "spin", "steps", "spin-steps", "none"],
                     help="device work enqueued just ahead of the start event: an untimed graph replay, a spin "
                          "kernel, (eager) untimed launches of the preceding buffer sets, or a spin long enough "
@@ -509,7 +513,7 @@ def time_steps(args, wl, dev, world, graph_ok=True):
             # (a profiler's per-dispatch interception makes submission ~10 us per launch,
             # slower than the kernels: without the spin the timed launches would trickle
             # in one by one), then the untimed launches of the preceding sets
-            torch.cuda._sleep(spin_cycles(30.0 * (args.steps + lead_n) + 200.0))
+            torch.cuda._sleep(spin_cycles(args.spin_us_per_launch * (args.steps + lead_n) + 200.0))
             for j in range(lead_n):
                 wl.step_call(j - lead_n)()
         elif graph is None and args.lead == "steps":
@@ -599,10 +603,17 @@ def c5_section(args, rank, world, dev, dt, code, cpu):
     over the ranks (one per GPU at N = 8), each rank's share one launch per step
     (the single-matrix entry at N = 8, the batched one below), quant statistics
     scattered from rank 0.  Aggregate = 8 matrices / the slowest rank's time."""
+    import copy
+
     import torch
 
     import workloads as W
 
+    # timed over max(K, C5_MIN_STEPS) steps: at the driver's K = 20 the first launches
+    # after the lead weigh 1-2 % of a 20-step region (78.5 % at K = 200 vs 76.7 % at
+    # K = 20 on one box, profiles/r04/final/); the headline keeps exactly K
+    args = copy.copy(args)
+    args.steps = max(args.steps, C5_MIN_STEPS)
     m, n = args.c5_shape
     all_mats = [[(g, m, n) for g in range(r, W.C5_MATRICES, world)] for r in range(world)]
     mats = all_mats[rank]

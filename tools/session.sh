@@ -98,7 +98,8 @@ for stage in "$@"; do
         trace configs_c5 nf4_flat_kernel 32 600 -- tools/bench_configs.py --configs c5
         trace bench_8192 nf4_flat_kernel 64 300 -- bench.py --m 8192 --n 8192 --steps 64 --no-cpu-baseline ;;
     rocprof)
-        trace bench nf4_flat_kernel 200 300 -- bench.py --steps 200 --no-cpu-baseline --no-c5 --no-cache-warm
+        trace bench nf4_flat_kernel 200 300 -- bench.py --steps 200 --no-cpu-baseline --no-c5 --no-cache-warm \
+            --spin-us-per-launch 150
         python3 tools/rocprof_summary.py "$O/prof_bench" nf4_flat_kernel "$O/rocprof_bench_summary.json" \
             "$O/rocprof_bench_kernel_stats.csv" --last 200 > /dev/null ;;
     pmc)  # headline HBM traffic (FETCH_SIZE / WRITE_SIZE passes, calibrated) + decode-GEMM SQ counters
