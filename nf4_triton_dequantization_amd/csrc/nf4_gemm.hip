@@ -8,16 +8,18 @@ namespace {
 
 using namespace nf4gemm;
 
-// Defaults, from tools/sweep_gemm.py on MI355X (profiles/r01/sweep_gemm.jsonl:
-// Llama-3-8B shapes and the grouped q/k/v and gate/up column totals, M = 1..32).
-// N = all columns of the launch (a grouped launch passes the sum).
-//  * M <= 8: the persistent streaming kernel whenever x[M][K] fits its LDS
-//    (falls back to the streaming kernel if absmax wraps inside a row), strips
-//    by width; long K (down projection): streaming, K split growing with M.
-//  * 8 < M <= 16: streaming with a 2-way K split and 4 strips per workgroup for
-//    wide N; the 128-deep kernel for narrow N and long K.
-//  * 16 < M <= 32: the 128-deep kernel with several strips per wave (x loads
-//    shared) and a K split where N alone cannot fill the chip.
+// Defaults, from tools/sweep_gemm.py on MI355X (Llama-3-8B shapes and the grouped
+// q/k/v and gate/up column totals, M = 1..32; re-checked in round 4,
+// profiles/r04/gemm/sweep_gemm_m1_12.jsonl, sweep_gemm_m16_32.jsonl: the default is
+// the fastest or within 2 % of it except where noted below).  N = all columns of the
+// launch (a grouped launch passes the sum).
+//  * M <= 8: the persistent kernel whenever x[M][K] fits its LDS (the streaming
+//    kernel if absmax wraps inside a row), strips by width.
+//  * 8 < M <= 16: the persistent kernel with K slices; the register-resident
+//    kernel for N <= 1024.
+//  * 16 < M <= 32: the register-resident kernel (two K slices at K = 4096; 16 waves
+//    and no slices for the widest launches at M <= 24); the 128-deep and
+//    shared-activation kernels where K % 256 != 0 or N < 1024.
 bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K);
 
 static nf4_gemm_cfg k128_cfg(int64_t M, int64_t N, int64_t K, int waves, int depth, int ksplit, int strips) {
@@ -54,11 +56,12 @@ static nf4_gemm_cfg nonpersist_cfg(int64_t M, int64_t N, int64_t K) {
         if (N < 4096) return k128_cfg(M, N, K, 4, 2, 4, 1);
         return k128_cfg(M, N, K, 8, 2, 1, 1);
     }
-    if (K % kSChunkK == 0 && N >= 2048) {
+    if (K % kSChunkK == 0 && N >= 1024) {
         // the register-resident kernel with pair-table lookups, 8 waves x 256-deep
         // chunks: per launch at M = 32 (profiles/r02/sweep_gemm_xr.jsonl) 20.4 vs 21.7 us
         // on 14336x4096, 11.9 vs 12.3 on 4096^2, 23.5 vs 24.6 on 4096x14336, 13.8 vs 14.2
-        // on grouped q/k/v (6144), 31.4 vs 37.2 on grouped gate/up (28672)
+        // on grouped q/k/v (6144), 31.4 vs 37.2 on grouped gate/up (28672); from N = 1024
+        // since round 4 (7.7 vs 8.6-9.0 us at M = 24 / 32, profiles/r04/gemm/sweep_gemm_m16_32.jsonl)
         if (M <= 24 && N >= 24576) {
             // the widest launches (grouped gate/up) at M <= 24: 16 waves span K = 4096,
             // no split-K hand-off: 26.0 vs 27.6 us (profiles/r04/gemm/xr_no_handoff_m24_m32.jsonl)
@@ -88,6 +91,13 @@ nf4_gemm_cfg default_gemm_cfg(int64_t M, int64_t N, int64_t K) {
         const nf4_gemm_cfg c{NF4DQ_GEMM_PERSIST, 8, 2, 1, strips};
         if (valid_gemm_cfg(c, M, N, K)) return c;
     } else if (K % kSChunkK == 0 && M <= 16) {
+        if (N <= 1024) {
+            // too few strips to cover the CUs with slices of the persistent kernel: the
+            // register-resident kernel, 6.6 vs 7.7 us on 1024x4096 at M = 12
+            // (profiles/r04/gemm/sweep_gemm_m1_12.jsonl)
+            const nf4_gemm_cfg c{NF4DQ_GEMM_XR, 8, 2, (int)((K / kChunkK + 15) / 16), 2};
+            if (valid_gemm_cfg(c, M, N, K)) return c;
+        }
         // persistent with K slices: the fewest slices whose x fits, while the
         // (strip group, slice) pairs still cover every CU
         for (int strips = 2; strips <= 4; strips *= 2)
