@@ -13,7 +13,6 @@
 //   ABL_NORING  ABL_NOWLOAD + ABL_NOSCALE: the ring issues no memory operation
 //   ABL_L2WIN   weight loads folded into a 256 KiB window (L2-resident, same instructions)
 //   ABL_SKELETON ABL_NORING + ABL_NOLUT + ABL_NOMMA: control flow, x staging, tables, VALU
-//   ABL_PKASM   pair products as one inline-asm v_pk_mul_f32 each (variant: correct results)
 //   ABL_PAIR    persistent kernel: two ring slots decoded step-interleaved (variant: correct results)
 //   ABL_EMPTY   persistent kernel: returns at entry (the launch of its grid, nothing else)
 //   ABL_NOLOOP  persistent kernel: no chunk loop (x staging, tables, outputs: the fixed cost)
@@ -25,9 +24,6 @@
 
 #if defined(ABL_NTW)  // weight loads with the nt (streaming) policy, as the flat dequant kernel's
 #define NF4_ABL_WLOAD(rsrc_, off_) __builtin_amdgcn_raw_buffer_load_b128((rsrc_), (off_), 0, 2)
-#endif
-#if defined(ABL_PKASM)  // a variant, not an ablation: correct results
-#define NF4_PK_ASM 1
 #endif
 #if defined(ABL_PAIR)  // a variant, not an ablation: correct results
 #define NF4_PERSIST_PAIR 1
