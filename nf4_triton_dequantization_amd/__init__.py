@@ -9,6 +9,7 @@ The alias package ``nf4_triton_dequantization`` (repo root) re-exports the same
 names so existing callers (benchmark.py:11) import it unchanged.
 """
 from .kernel import (  # noqa: F401
+    check_gemm_workspaces,
     dequantize_nf4_bnb,
     dequantize_nf4_into,
     dequantize_nf4_many,
@@ -21,6 +22,6 @@ from .bnb_layout import Linear4bit, Params4bit, QuantState, quantize_nf4  # noqa
 from .checkpoint import load_nf4_safetensors, save_nf4_safetensors  # noqa: F401
 
 __all__ = ["triton_dequantize_nf4", "reset_triton_dequantize_state", "dequantize_nf4_many",
-           "dequantize_nf4_bnb", "dequantize_nf4_into", "nf4_linear", "nf4_linear_grouped", "Linear4bit",
+           "dequantize_nf4_bnb", "dequantize_nf4_into", "nf4_linear", "nf4_linear_grouped", "check_gemm_workspaces", "Linear4bit",
            "Params4bit", "QuantState", "quantize_nf4", "load_nf4_safetensors", "save_nf4_safetensors"]
 __version__ = "0.1.0"

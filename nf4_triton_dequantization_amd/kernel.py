@@ -421,6 +421,25 @@ def _gemm_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     return ws
 
 
+def check_gemm_workspaces() -> None:
+    """Raise if a fused-GEMM split-K reduction gave up waiting since the last check.
+
+    Waits for every stream that owns one of ``nf4_linear``'s cached workspaces and reads
+    its sticky error word (``nf4_gemm_check_workspace``); a stalled K slice
+    makes the reducer emit NaN for the missing partial and set the word.  The library
+    re-zeroes such a workspace, so the next call starts clean.  Raises RuntimeError
+    naming the device and stream; returns None when every workspace is clean.
+    """
+    bad = []
+    L = _lib.lib() if _GEMM_WS else None
+    for (dev_index, stream), ws in list(_GEMM_WS.items()):
+        rc = L.nf4_gemm_check_workspace(ws.data_ptr(), ws.numel(), stream)
+        if rc:
+            bad.append(f"cuda:{dev_index} stream {stream:#x}: {_lib.strerror(rc)}")
+    if bad:
+        raise RuntimeError("nf4 fused GEMM: " + "; ".join(bad))
+
+
 def nf4_linear(x: torch.Tensor, module, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``x @ W.t() (+ bias)`` for an NF4 ``Linear4bit`` weight W (reference semantics).
 

@@ -61,6 +61,18 @@ def test_check_workspace_host_validation():
     assert L.nf4_gemm_check_workspace(FAKE, 1024, None) == _lib.ERR_ARG
 
 
+def test_check_gemm_workspaces_without_workspaces():
+    """The Python check has nothing to report before any fused-GEMM call (no device call)."""
+    from nf4_triton_dequantization_amd import check_gemm_workspaces, kernel
+
+    saved = dict(kernel._GEMM_WS)
+    kernel._GEMM_WS.clear()
+    try:
+        assert check_gemm_workspaces() is None
+    finally:
+        kernel._GEMM_WS.update(saved)
+
+
 FAKE = 0x1000  # never dereferenced: every call below fails validation first
 
 

@@ -162,6 +162,20 @@ def test_workspace_reuse_across_shapes(coracle, gpu):
         _check(nf4_linear(xt.to(gpu), mod), xb, W, "bf16")
 
 
+def test_check_gemm_workspaces_after_split_k(coracle, gpu):
+    """nf4_linear's cached workspaces read clean after split-K launches (M = 16: the
+    persistent kernel's K slices; M = 32: the register-resident kernel's two slices)."""
+    from nf4_triton_dequantization_amd import check_gemm_workspaces, nf4_linear
+
+    for (M, N, K) in [(16, 4096, 4096), (32, 2048, 4096), (12, 1024, 4096)]:
+        packed, a1, a2 = O.make_inputs(N, K, seed=3 * N + M)
+        W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16)
+        mod = make_module(packed, a1, a2, N, K, "bf16", gpu)
+        xt, xb = _x_bits(M, K, "bf16", seed=M + 7)
+        _check(nf4_linear(xt.to(gpu), mod), xb, W, "bf16")
+        assert check_gemm_workspaces() is None
+
+
 def _gemm_cfg_call(L, _lib, xt, mod_t, y, dt_code, N, K, cfg):
     import ctypes
 
