@@ -1,0 +1,122 @@
+"""Soak test of the fused GEMM's split-K hand-offs (tools only; measurement hygiene).
+
+    python tools/soak_gemm.py [--iters 300] [--seconds 480] > soak.jsonl
+
+Every kernel form that meets across workgroups is launched `iters` times back to back
+on one workspace: the persistent kernel's K slices (ticket and exchange forms), the
+register-resident kernel's two-slice exchange and seven-slice tickets, the
+streaming / 128-deep / shared-activation kernels' ticket reductions, and the balanced
+kernel.  Every launch's output must be bitwise equal to the first launch's (the
+hand-offs sum in a fixed order, so the result is reproducible), the workspace error
+word must stay clear (nf4_gemm_check_workspace after every 50 launches and at the
+end), and the workspace body must be all zero at the end.  One JSON line per
+configuration (progress), then a summary line.  Each case also checks its first output
+against a float64 product of the oracle's weights (the GEMM suite's tolerance).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+from nf4_triton_dequantization_amd import _lib  # noqa: E402
+import nf4_oracle as O  # noqa: E402  -- the checker
+
+G = _lib
+CASES = [  # (label, M, N, K, cfg or None for the library default)
+    ("persist ksplit 2 (exchange)", 16, 4096, 4096, G.GemmCfg(G.GEMM_PERSIST, 8, 2, 2, 2)),
+    ("persist ksplit 4 (tickets)", 12, 4096, 4096, G.GemmCfg(G.GEMM_PERSIST, 8, 2, 4, 4)),
+    ("xr two slices, unrolled groups", 32, 14336, 4096, G.GemmCfg(G.GEMM_XR, 8, 2, 2, 2)),
+    ("xr two slices, grouped gate/up width", 32, 28672, 4096, G.GemmCfg(G.GEMM_XR, 8, 2, 2, 2)),
+    ("xr seven slices (tickets)", 24, 4096, 14336, G.GemmCfg(G.GEMM_XR, 8, 2, 7, 2)),
+    ("stream ksplit 4", 8, 4096, 4096, G.GemmCfg(G.GEMM_STREAM, 8, 2, 4, 4)),
+    ("k128 ksplit 4", 32, 2048, 4096, G.GemmCfg(G.GEMM_K128, 8, 1, 4, 4)),
+    ("xs (shared activation) ksplit 4", 32, 6144, 4096, G.GemmCfg(G.GEMM_XS, 4, 8, 4, 1)),
+    ("balanced (stream-K)", 1, 14336, 4096, G.GemmCfg(G.GEMM_SK, 8, 0, 1, 0)),
+    ("library default M = 32", 32, 14336, 4096, None),
+    ("library default M = 16", 16, 14336, 4096, None),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=300)
+    ap.add_argument("--seconds", type=float, default=480.0, help="stop starting new cases after this")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    L = _lib.lib()
+    st = torch.cuda.current_stream()
+    orc = O.COracle()
+    orc.set_threads(16)
+    t_start = time.time()
+    total = {"cases": 0, "launches": 0, "mismatches": 0, "timeouts": 0, "dirty_workspaces": 0, "oracle_fail": 0}
+    for label, M, N, K, cfg in CASES:
+        if time.time() - t_start > args.seconds:
+            break
+        packed, a1, a2 = O.make_inputs(N, K, seed=N + K + M, a2_kind="normal")
+        q, t1, t2 = (torch.from_numpy(packed).to(dev), torch.from_numpy(a1).to(dev), torch.from_numpy(a2).to(dev))
+        x = torch.from_numpy(O.normal_f32(M + 11, M * K, stream=9).reshape(M, K)).to(torch.bfloat16)
+        xd = x.to(dev)
+        y = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+        cp = ctypes.byref(cfg) if cfg is not None else None
+        wsz = L.nf4_gemm_workspace_bytes_cfg(M, N, K, cp) if cfg is not None else L.nf4_gemm_workspace_bytes(M, N, K)
+        ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=dev)
+        wptr = ws.data_ptr() if wsz else None
+
+        def launch():
+            return L.nf4_gemm_ref_cfg(xd.data_ptr(), M, q.data_ptr(), q.numel(), t1.data_ptr(), t1.numel(),
+                                      t2.data_ptr(), t2.numel(), y.data_ptr(), _lib.BF16, N, K, wptr, wsz, cp,
+                                      st.cuda_stream)
+
+        rc = launch()
+        if rc:
+            print(json.dumps({"case": label, "skipped": _lib.strerror(rc)}), flush=True)
+            continue
+        torch.cuda.synchronize()
+        first = y.clone()
+        # oracle check of the first output (float64 product of the reference's weights)
+        w = orc.dequant_ref(packed, a1, a2, N, K, O.BF16)
+        wf = (w.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+        xf = x.float().numpy().astype(np.float64)
+        ref = xf @ wf.T
+        mag = np.abs(xf) @ np.abs(wf).T
+        got = first.float().cpu().numpy().astype(np.float64)
+        ok_oracle = bool((np.abs(got - ref) <= 2.0 ** -8 * np.abs(ref) + 2.0 ** -20 * mag + 2.0 ** -134).all())
+        mism = tmo = 0
+        t0 = time.time()
+        for i in range(args.iters):
+            y.fill_(0)  # a launch that writes nothing shows up as a mismatch
+            assert launch() == 0
+            mism += int(not torch.equal(y.view(torch.int16), first.view(torch.int16)))
+            if wsz and ((i + 1) % 50 == 0 or i + 1 == args.iters):
+                tmo += int(L.nf4_gemm_check_workspace(wptr, wsz, st.cuda_stream) == _lib.ERR_SPLITK_TIMEOUT)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        # the body after the counters + header must be all zero between calls
+        dirty = int(wsz > 0 and bool(ws.any().item()))
+        line = {"case": label, "M": M, "N": N, "K": K,
+                "cfg": None if cfg is None else [cfg.kernel, cfg.waves, cfg.depth, cfg.ksplit, cfg.strips],
+                "launches": args.iters, "bitwise_checks": args.iters,
+                "mismatches": mism, "timeouts": tmo, "workspace_dirty": dirty, "oracle_ok": ok_oracle,
+                "us_per_launch": round(dt / args.iters * 1e6, 2)}
+        print(json.dumps(line), flush=True)
+        total["cases"] += 1
+        total["launches"] += args.iters
+        total["mismatches"] += mism
+        total["timeouts"] += tmo
+        total["dirty_workspaces"] += dirty
+        total["oracle_fail"] += int(not ok_oracle)
+    print(json.dumps({"summary": total, "seconds": round(time.time() - t_start, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
