@@ -142,6 +142,12 @@ for l in open(sys.argv[1]):
     gemmpass)  # the Llama-3-8B decode pass, fused GEMM (tools/bench_gemm.py)
         timeout -k 10 500 $PY tools/bench_gemm.py --ms ${GEMM_MS:-1,4,8,12,16,24,32} > "$O/bench_gemm.jsonl" 2> "$O/bench_gemm.err"
         cat "$O/bench_gemm.jsonl" ;;
+    gemmtrace)  # kernel trace + stats of the fused decode pass (grouped form only), GEMM_MS (default 1,32)
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_gemm" -o gemm -- \
+            python3 -u tools/bench_gemm.py --ms ${GEMM_MS:-1,32} --no-bf16 --no-composite > "$O/gemmtrace.out" 2> "$O/gemmtrace.err"
+        find "$O/prof_gemm" -name "*kernel_stats.csv" -exec cp {} "$O/gemm_kernel_stats.csv" \;
+        rm -rf "$O/prof_gemm"
+        cat "$O/gemm_kernel_stats.csv" ;;
     configs)
         timeout -k 10 900 $PY tools/bench_configs.py > "$O/configs.jsonl" 2> "$O/configs.err"; cat "$O/configs.jsonl" ;;
     *)
