@@ -162,6 +162,20 @@ def test_workspace_reuse_across_shapes(coracle, gpu):
         _check(nf4_linear(xt.to(gpu), mod), xb, W, "bf16")
 
 
+@pytest.mark.parametrize("M,N,K", [(12, 1024, 4096), (16, 1024, 4096), (20, 28672, 4096), (24, 24576, 4096)])
+def test_round4_default_rules(coracle, gpu, M, N, K):
+    """The library defaults added in round 4: the register-resident kernel for
+    1024-column launches at 8 < M <= 16, and its 16-wave whole-K form for the widest
+    launches at 16 < M <= 24 (default_gemm_cfg / nonpersist_cfg)."""
+    from nf4_triton_dequantization_amd import nf4_linear
+
+    packed, a1, a2 = O.make_inputs(N, K, seed=5 * N + M, a2_kind="normal")
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16)
+    mod = make_module(packed, a1, a2, N, K, "bf16", gpu)
+    xt, xb = _x_bits(M, K, "bf16", seed=M + 19)
+    _check(nf4_linear(xt.to(gpu), mod), xb, W, "bf16")
+
+
 def test_check_gemm_workspaces_after_split_k(coracle, gpu):
     """nf4_linear's cached workspaces read clean after split-K launches (M = 16: the
     persistent kernel's K slices; M = 32: the register-resident kernel's two slices)."""
