@@ -1461,7 +1461,9 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_stream_kernel(const StreamArg
     const uint32_t sg = sgi - Mt.sg_begin;
     const uint32_t strip = sg * A.T + wave % A.T, part = wave / A.T;
     const uint32_t row = strip * 16u + nl;
-    const uint32_t s0 = ks * A.cps;
+    // an empty last slice (ksplit * cps > chunks, e.g. 5 chunks in 4 slices of 2): s0 is
+    // clamped, so the slice has no chunks, contributes zero partials and takes its ticket
+    const uint32_t s0r = ks * A.cps, s0 = s0r < A.chunks ? s0r : A.chunks;
     const uint32_t s1 = s0 + A.cps < A.chunks ? s0 + A.cps : A.chunks;
     const uint32_t nloc = s1 - s0;
     const uint32_t l0 = part * A.cpp;  // first chunk of this wave within the slice

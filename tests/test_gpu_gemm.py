@@ -162,6 +162,33 @@ def test_workspace_reuse_across_shapes(coracle, gpu):
         _check(nf4_linear(xt.to(gpu), mod), xb, W, "bf16")
 
 
+@pytest.mark.parametrize("M,N,K,cfg", [(8, 2560, 1280, (2, 4, 4, 4, 1)), (12, 384, 1280, (2, 4, 2, 4, 1)),
+                                       (3, 256, 1792, (2, 8, 2, 6, 2)), (20, 128, 1792, (2, 8, 2, 5, 1))])
+def test_streaming_kernel_empty_last_slices(coracle, gpu, M, N, K, cfg):
+    """ksplit * ceil(chunks / ksplit) > chunks leaves the last slice(s) without chunks:
+    they must add zero partials and take their tickets (found by tools/fuzz_gemm.py:
+    the slice's range underflowed and its waves read past the staged x into NaN)."""
+    import ctypes
+
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    packed, a1, a2 = O.make_inputs(N, K, seed=N + K + M, a2_kind="normal")
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16)
+    xt, xb = _x_bits(M, K, "bf16", seed=M + 3)
+    mod_t = (torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu))
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=gpu)
+    c = _lib.GemmCfg(*cfg)
+    wsz = L.nf4_gemm_workspace_bytes_cfg(M, N, K, ctypes.byref(c))
+    ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=gpu)
+    rc = L.nf4_gemm_ref_cfg(xt.to(gpu).data_ptr(), M, mod_t[0].data_ptr(), mod_t[0].numel(), mod_t[1].data_ptr(),
+                            mod_t[1].numel(), mod_t[2].data_ptr(), mod_t[2].numel(), y.data_ptr(), _lib.BF16, N, K,
+                            ws.data_ptr(), wsz, ctypes.byref(c), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, _lib.strerror(rc)
+    assert L.nf4_gemm_check_workspace(ws.data_ptr(), wsz, torch.cuda.current_stream().cuda_stream) == 0
+    _check(y, xb, W, "bf16")
+
+
 @pytest.mark.parametrize("M,N,K", [(12, 1024, 4096), (16, 1024, 4096), (20, 28672, 4096), (24, 24576, 4096)])
 def test_round4_default_rules(coracle, gpu, M, N, K):
     """The library defaults added in round 4: the register-resident kernel for
