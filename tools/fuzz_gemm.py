@@ -5,9 +5,11 @@
 Each case draws M (1-32), N (a multiple of 64 up to 3072), K (a multiple of 128 up to
 6144), the dtype (bf16 / fp16), full or short absmax arrays (the reference's repeat-wrap)
 and signed nested absmax. It then runs ``nf4_linear`` (the library's choice of kernel
-and decomposition) and, for one case in four, an explicitly drawn valid configuration
-through ``nf4_gemm_ref_cfg``. The result is checked against a float64 product of the C
-oracle's dequantized weights with the GEMM suite's tolerance
+and decomposition) and, for a share of the cases (``--cfg-rate``), an explicitly drawn
+configuration of any of the six kernels through ``nf4_gemm_ref_cfg`` (invalid draws are
+skipped; a split-K timeout flagged in the workspace counts as a failure). Each result is
+checked against a float64 product of the C oracle's dequantized weights with the GEMM
+suite's tolerance
 (tests/test_gpu_gemm.py: 2^-p |ref| + 2^-20 sum|x w|). One progress line per 100
 cases, then a summary.
 """
@@ -44,8 +46,10 @@ def tol(ref, mag, dt):
 
 
 def random_cfg(rng, M, N, K):
-    """A drawn configuration of one of the five tuning kernels (may be invalid: skipped)."""
-    k = int(rng.integers(1, 6))
+    """A drawn configuration of one of the six kernels (may be invalid: skipped)."""
+    k = int(rng.integers(1, 7))
+    if k == _lib.GEMM_SK:  # balanced kernel: 8 waves, ring depth 0/2/4/8, no slices
+        return _lib.GemmCfg(k, 8, int(rng.choice([0, 2, 4, 8])), 1, 0)
     waves = int(rng.choice([4, 8, 16]))
     depth = int(rng.choice([1, 2, 4, 8]))
     strips = int(rng.choice([1, 2, 4]))
@@ -65,6 +69,7 @@ def main():
     ap.add_argument("--cases", type=int, default=1500)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--seconds", type=float, default=500.0)
+    ap.add_argument("--cfg-rate", type=float, default=0.25, help="share of cases that also run a drawn configuration")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     L = _lib.lib()
@@ -94,7 +99,7 @@ def main():
         bound = tol(ref, np.abs(xf) @ np.abs(wf).T, dt)
         mod = make_module(p, a1, a2, N, K, dt, dev)
         outs = [("default", nf4_linear(xt.to(dev), mod))]
-        if rng.random() < 0.25:
+        if rng.random() < args.cfg_rate:
             cfg = random_cfg(rng, M, N, K)
             wsz = L.nf4_gemm_workspace_bytes_cfg(M, N, K, ctypes.byref(cfg))
             ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=dev)
@@ -108,7 +113,11 @@ def main():
                                     torch.cuda.current_stream().cuda_stream)
             if rc == 0:
                 cfg_runs += 1
-                outs.append(([cfg.kernel, cfg.waves, cfg.depth, cfg.ksplit, cfg.strips], y))
+                label = [cfg.kernel, cfg.waves, cfg.depth, cfg.ksplit, cfg.strips]
+                if wsz and L.nf4_gemm_check_workspace(ws.data_ptr(), wsz, torch.cuda.current_stream().cuda_stream):
+                    bad += 1
+                    print(json.dumps({"timeout": {"M": M, "N": N, "K": K, "cfg": label, "seed": seed}}), flush=True)
+                outs.append((label, y))
         for label, y in outs:
             got = bits_to_f64(y.contiguous().view(torch.int16).cpu().numpy().view(np.uint16), dt).reshape(M, N)
             if not (np.abs(got - ref) <= bound).all():
