@@ -18,39 +18,42 @@ NF4->bf16 (configs[1]).  A *step* is one pass of the hot path over one batch:
 before this process touches the GPU and relays rank 0's line; under a launcher
 WORLD_SIZE must equal N.
 
-Timed region (``value``): K steps as K eager launches of the product C-ABI entry
-(``nf4_dequant_ref``, arguments prepared up front), bracketed by barrier +
-synchronize on both sides, HIP events on the launch stream around them.  Ahead of
-the start event sit L = 16 untimed launches of the preceding buffer sets, so the
-queue holds real work when timing starts, as in a steady stream of weights, and
-ahead of those a device spin that outlasts the host's submission of all L + K
-launches (``--lead spin-steps``): the K kernels then run back to back even when
-a profiler's per-dispatch interception makes the host slower than the GPU (a
-kernel trace without it showed host-bound gaps and per-kernel times 11 % above
-the events' figure); before that, one untimed launch per buffer set warms
-the GPU TLB for every set.  ``--launch graph`` captures the K steps into one
-hipGraph instead: on ROCm 7.2 a replay carries a fixed ~7-10 us outside the
-kernels (rocprof: 20 launches span 139 us, the events 149 us), 0.4-0.5 us per
-step at the driver's K = 20 (A/B: profiles/r02/bench_eager_ab.txt).  Step i uses
-input set i % Pin and output set i % Pout, rotated independently: Pin so that each
-rank's distinct READ bytes (packed weights + statistics) span >= 512 MiB -- 2x the
-256 MiB Infinity Cache, so every weight comes from HBM as in a model pass
-(profiles/r04/cache/cache_ab_4096.jsonl: the launch time depends on the distinct
-reads only; below ~256 MB the weights are re-read from the Infinity Cache) -- and
-Pout so that the outputs span >= 512 MiB; under graph replay Pin also keeps a set's
-reuse >= 512 MiB of reads apart across the untimed -> timed boundary (a
-scratch-write flush instead costs 1-2 us per step through TLB misses,
-profiles/r02/bench_ab.txt).  ``value`` = elements of all ranks / max over ranks of
-the region time.  ``cache_warm`` (c2): the same timing over the round-1..3 rotation
-(13 full sets, 112 MB of reads: Infinity-Cache-resident weights), reported beside
-the headline, never as ``value``.
+Timed regions (``value``): R = ``--repeats`` (default 5) regions of exactly K steps,
+each K eager launches of the product C-ABI entry (``nf4_dequant_ref``, arguments
+prepared up front), bracketed by barrier + synchronize on both sides, HIP events on the
+launch stream around them.  Per region the max over ranks counts; the region with the
+median of those maxima is the result (median, not one sample), and every
+region's figure is on the line (``repeats``).  Ahead of each start event sit L = 16
+untimed launches of the preceding buffer sets, so the queue holds real work when
+timing starts, as in a steady stream of weights, and ahead of those a device spin that
+outlasts the host's submission of all L + K launches (``--lead spin-steps``): the K
+kernels then run back to back even when a profiler's per-dispatch interception makes
+the host slower than the GPU (a kernel trace without it showed host-bound gaps and
+per-kernel times 11 % above the events' figure); before that, one untimed launch per
+buffer set warms the GPU TLB for every set.  ``--launch graph`` captures the K steps
+into one hipGraph instead: on ROCm 7.2 a replay carries a fixed ~7-10 us outside the
+kernels (rocprof: 20 launches span 139 us, the events 149 us), 0.4-0.5 us per step at
+the driver's K = 20 (A/B: profiles/r02/bench_eager_ab.txt).  Step i uses input set
+i % Pin and output set i % Pout, rotated independently: Pin so that each rank's
+distinct READ bytes (packed weights + statistics) span >= 512 MiB -- 2x the 256 MiB
+Infinity Cache, so every weight comes from HBM as in a model pass
+(profiles/r04/cache/cache_ab_4096.jsonl: the launch time depends on the distinct reads
+only; below ~256 MB the weights are re-read from the Infinity Cache) -- and Pout so
+that the outputs span >= 512 MiB; under graph replay Pin also keeps a set's reuse
+>= 512 MiB of reads apart across the untimed -> timed boundary (a scratch-write flush
+instead costs 1-2 us per step through TLB misses, profiles/r02/bench_ab.txt).
+``value`` = elements of all ranks / the median region's time.
 
 Roofline (``roofline``): ``achieved`` = algorithmic bytes per launch (SURVEY
-§8d: N/2 packed + 2N out + nb absmax + 4*min(n2, m*G) nested absmax) / mean
-launch duration = HIP-event time of the timed region on the launch stream / K
-(inter-launch gaps count against us); ``peak`` = 8 TB/s; ``traffic`` =
-PMC-counted HBM bytes per launch from profiles/<round>/pmc_traffic.json
-(tools/pmc_traffic.py) when present for this shape.
+§8d: N/2 packed + 2N out + nb absmax + 4*min(n2, m*G) nested absmax) / launch
+duration = HIP-event time of the median region on the launch stream / K
+(inter-launch gaps count against us; min / median / max over the regions beside it);
+``peak`` = 8 TB/s; ``traffic`` = PMC-counted HBM bytes per launch from
+profiles/<round>/pmc_traffic.json (tools/pmc_traffic.py) when present for this shape.
+``ceiling_measured``: the memory-system twin of the same launch (the flat kernel's
+loads and stores over the same tile grid, no decode: tools/stream_probe.hip), timed
+right after the headline by the same method on the same rotation -- what this access
+pattern gets from the memory system on this box, and the kernel's distance from it.
 
 CPU baseline (``cpu_baseline``, rank 0 at N=1), same workload on this GPU's
 host share of cores (at most 16): ``value`` = oracle/fallback_torch.py, a
@@ -64,9 +67,11 @@ same at 1 thread.
 the spawn / gloo / max-over-ranks path without a GPU.
 
 Multi-GPU: every rank dequantizes its own matrices; rank 0 owns the quant
-statistics of every rank's matrices and broadcasts them once over RCCL at setup
-(sharding.broadcast_quant_stats, timed and reported separately) -- no
-collective on the data path.
+statistics of every rank's matrices and scatters them once over RCCL at setup, each
+rank receiving only its own matrices' statistics (sharding.scatter_quant_stats, timed
+and reported separately as ``quant_state_scatter_ms``) -- no collective on the data
+path.  ``--dist-backend nccl`` at N = 1 forms a one-rank group, so the scatter runs
+over RCCL on a single GPU as well.
 """
 from __future__ import annotations
 
@@ -85,7 +90,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_HBM = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md)
-ROUNDS = ("r04", "r03", "r02", "r01")  # profiles/<round>/pmc_traffic.json, newest first
+ROUNDS = ("r05", "r04", "r03", "r02", "r01")  # profiles/<round>/pmc_traffic.json, newest first
 # Rotation (round 4, profiles/r04/cache/cache_ab_4096.jsonl): input sets (packed weight +
 # absmax + nested absmax) and output sets rotate independently.  The per-launch time
 # depends on the distinct READ bytes only: at 4096^2 6.89 us while they stay <= 225 MB
@@ -94,11 +99,8 @@ ROUNDS = ("r04", "r03", "r02", "r01")  # profiles/<round>/pmc_traffic.json, newe
 # written bytes change nothing from 67 MB to 2 GB.  A streamed model's weights are read
 # once per pass, so the headline rotates >= 512 MiB of distinct input bytes per rank
 # (2x the Infinity Cache: every weight read comes from HBM) and >= 512 MiB of outputs.
-# The cache-warm figure (the round-1..3 rotation, 13 full sets: 112 MB of reads) is
-# reported beside it, never as `value`.
 MIN_READ_FOOTPRINT = 512 << 20
 MIN_WRITE_FOOTPRINT = 512 << 20
-CACHE_WARM_SETS = 13
 C5_MIN_STEPS = 100  # the c5 object's timed steps at least (its launches are 27-215 us)
 
 
@@ -120,7 +122,10 @@ def parse_args(argv=None):
                     help="rotating input sets (0 = enough for >= 512 MiB of distinct reads per rank)")
     ap.add_argument("--out-sets", type=int, default=0,
                     help="rotating output sets (0 = enough for >= 512 MiB of distinct writes per rank)")
-    ap.add_argument("--no-cache-warm", action="store_true", help="skip the cache-warm figure")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="timed regions of K steps each (the median region is the result, SURVEY 8d)")
+    ap.add_argument("--no-ceiling", action="store_true",
+                    help="skip the memory-system twin (roofline.ceiling_measured)")
     ap.add_argument("--launch", default="eager", choices=["eager", "graph"],
                     help="timed steps as eager C-ABI launches (default) or one hipGraph replay")
     ap.add_argument("--no-graph", action="store_true", help="same as --launch eager (kept for old scripts)")
@@ -446,8 +451,10 @@ class Workload:
 
 
 def time_steps(args, wl, dev, world, graph_ok=True):
-    """Warmup, one untimed pass over every buffer set, then the timed region (see the
-    module docstring); returns (ms for K steps on this rank, launch mode)."""
+    """Warmup, one untimed pass over every buffer set, then ``--repeats`` timed regions
+    of exactly K steps each (see the module docstring), every region bracketed by a
+    barrier + synchronize on both sides; returns ([ms for K steps on this rank, one per
+    region], launch mode)."""
     import torch
     import torch.distributed as dist
 
@@ -487,68 +494,136 @@ def time_steps(args, wl, dev, world, graph_ok=True):
         del scratch
     if not cpu and args.lead == "spin-steps":
         _spin_rate_calibrate()
-    if world > 1:
-        dist.barrier()
+    times = []
+    calls = [wl.step_call(i) for i in range(args.steps)] if not cpu else None  # bound before anything is timed
     if not cpu:
-        torch.cuda.synchronize()
-    if cpu:
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            wl.launch(i)
-        t_ms = (time.perf_counter() - t0) * 1e3
-    else:
         main_stream = torch.cuda.current_stream(dev)
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
-        calls = [wl.step_call(i) for i in range(args.steps)]  # bound before anything is timed
-        if graph is not None and args.lead == "replay":
-            # one more untimed replay enqueued right ahead of the start event: the
-            # timed steps follow warm steps back to back (as in a steady stream of
-            # work) and the host's submission of the timed replay hides behind it
-            graph.replay()
-        elif args.lead == "spin":
-            torch.cuda._sleep(100_000)  # device spin: hides only the host's submission
-        elif graph is None and args.lead == "spin-steps":
-            # a device spin that outlasts the host's submission of every launch below
-            # (a profiler's per-dispatch interception makes submission ~10 us per launch,
-            # slower than the kernels: without the spin the timed launches would trickle
-            # in one by one), then the untimed launches of the preceding sets
-            torch.cuda._sleep(spin_cycles(args.spin_us_per_launch * (args.steps + lead_n) + 200.0))
-            for j in range(lead_n):
-                wl.step_call(j - lead_n)()
-        elif graph is None and args.lead == "steps":
-            # untimed launches of the sets just before the timed ones (steps -L..-1):
-            # the queue holds real work when the start event fires, as in a steady
-            # stream of weights, so host launch latency never idles the GPU
-            for j in range(lead_n):
-                wl.step_call(j - lead_n)()
-        ev0.record(main_stream)
-        if graph is not None:
-            graph.replay()
+    for _rep in range(max(1, args.repeats)):
+        if world > 1:
+            dist.barrier()
+        if not cpu:
+            torch.cuda.synchronize()
+        if cpu:
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                wl.launch(i)
+            times.append((time.perf_counter() - t0) * 1e3)
         else:
-            for c in calls:
-                c()
-        ev1.record(main_stream)
-        torch.cuda.synchronize()
-        t_ms = ev0.elapsed_time(ev1)
-    if world > 1:
-        dist.barrier()
+            if graph is not None and args.lead == "replay":
+                # one more untimed replay enqueued right ahead of the start event: the
+                # timed steps follow warm steps back to back (as in a steady stream of
+                # work) and the host's submission of the timed replay hides behind it
+                graph.replay()
+            elif args.lead == "spin":
+                torch.cuda._sleep(100_000)  # device spin: hides only the host's submission
+            elif graph is None and args.lead == "spin-steps":
+                # a device spin that outlasts the host's submission of every launch below
+                # (a profiler's per-dispatch interception makes submission ~10 us per launch,
+                # slower than the kernels: without the spin the timed launches would trickle
+                # in one by one), then the untimed launches of the preceding sets
+                torch.cuda._sleep(spin_cycles(args.spin_us_per_launch * (args.steps + lead_n) + 200.0))
+                for j in range(lead_n):
+                    wl.step_call(j - lead_n)()
+            elif graph is None and args.lead == "steps":
+                # untimed launches of the sets just before the timed ones (steps -L..-1):
+                # the queue holds real work when the start event fires, as in a steady
+                # stream of weights, so host launch latency never idles the GPU
+                for j in range(lead_n):
+                    wl.step_call(j - lead_n)()
+            ev0.record(main_stream)
+            if graph is not None:
+                graph.replay()
+            else:
+                for c in calls:
+                    c()
+            ev1.record(main_stream)
+            torch.cuda.synchronize()
+            times.append(ev0.elapsed_time(ev1))
+        if world > 1:
+            dist.barrier()
     mode = "hipGraph" if graph is not None else ("host loop" if cpu else "eager")
-    return t_ms, mode
+    return times, mode
 
 
-def gather_times(my_ms, dev, world):
-    """(max over ranks, every rank's figure)."""
+def median_region(my_times, dev, world):
+    """The result of R timed regions: per region the max over ranks (the slowest rank
+    decides), then the region with the median of those maxima.  Returns (its time,
+    every rank's time in that region, the per-region maxima in region order)."""
+    R = len(my_times)
     if world == 1:
-        return my_ms, [my_ms]
-    import torch.distributed as dist
+        maxima, table = list(my_times), [list(my_times)]
+    else:
+        import torch.distributed as dist
 
-    from nf4_triton_dequantization_amd.sharding import max_over_ranks
+        from nf4_triton_dequantization_amd.sharding import max_over_ranks
 
-    t = max_over_ranks(my_ms, dev)
-    gathered = [None] * world
-    dist.all_gather_object(gathered, my_ms)
-    return t, gathered
+        maxima = [max_over_ranks(t, dev) for t in my_times]
+        table = [None] * world
+        dist.all_gather_object(table, list(my_times))
+    order = sorted(range(R), key=lambda i: maxima[i])
+    pick = order[(R - 1) // 2]  # the lower median for even R: always one measured region
+    return maxima[pick], [table[r][pick] for r in range(world)], maxima
+
+
+class TwinWorkload:
+    """The memory-system twin of a one-matrix step (tools/stream_probe.hip ``twin_mix``):
+    the flat kernel's packed-weight loads (4 B/lane, nt) and output stores (16 B/lane,
+    sc1 + nt) over the same tile grid, no decode and no scale loads, on the same
+    rotation rule (>= 512 MiB of distinct reads, >= 512 MiB of distinct writes)."""
+
+    cpu = False
+
+    def __init__(self, lib, m, n, dev):
+        import torch
+
+        self.L, self.nbytes = lib, m * n // 2
+        pin, pout = rotation_sets([(0, m, n)])
+        self.Pin, self.Pout, self.P = pin, pout, max(pin, pout)
+        self.ins = [torch.randint(0, 256, (self.nbytes,), dtype=torch.uint8, device=dev) for _ in range(pin)]
+        self.outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(pout)]
+        self.sink = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+        self.sp = torch.cuda.current_stream(dev).cuda_stream
+
+    def step_call(self, i):
+        a, b = self.ins[i % self.Pin].data_ptr(), self.outs[i % self.Pout].data_ptr()
+
+        def call(L=self.L, a=a, b=b):
+            rc = L.twin_launch(0, 2, 18, 1, a, self.nbytes, b, self.sink.data_ptr(), self.sp)
+            if rc:
+                raise RuntimeError(f"twin_launch: {rc}")
+        return call
+
+    def launch(self, i):
+        self.step_call(i)()
+
+
+def twin_ceiling(args, mat, dev, world, rank, alg, kernel_us):
+    """Time the twin of this rank's step exactly as the headline (same K, repeats, lead,
+    spin): the fastest this launch's access pattern runs on this box, and the product
+    kernel's distance from it."""
+    import torch
+
+    path = os.path.join(REPO, "tools", "_build", "libstreamprobe.so")
+    if not os.path.exists(path):
+        log("bench.py: tools/_build/libstreamprobe.so missing; no measured ceiling")
+        return None
+    L = ctypes.CDLL(path)
+    L.twin_launch.restype = ctypes.c_int
+    L.twin_launch.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_void_p]
+    _, m, n = mat
+    tw = TwinWorkload(L, m, n, dev)
+    times, _ = time_steps(args, tw, dev, world, graph_ok=False)
+    _, per, _ = median_region(times, dev, world)
+    us = per[rank] * 1e3 / args.steps
+    del tw
+    torch.cuda.empty_cache()
+    return {"kernel": "twin_mix (tools/stream_probe.hip): the flat kernel's loads and stores, no decode",
+            "launch_us": us, "achieved": alg / (us * 1e-6) / 1e9, "frac": alg / (us * 1e-6) / PEAK_HBM,
+            "kernel_over_twin": kernel_us / us,
+            "method": "same rotation, K, repeats, lead and spin as the headline, timed right after it"}
 
 
 def distribute_stats(all_mats, rank, world, dev, dt, cpu):
@@ -576,9 +651,10 @@ def distribute_stats(all_mats, rank, world, dev, dt, cpu):
                                       torch.from_numpy(W.uniform_f32(seed, (nb + 255) // 256, 1e-3, 1e-2,
                                                                      stream=3)), dt))
             per_rank.append(row)
-    if world == 1:
-        return [QuantStats(s.m, s.n, s.absmax.to(dev), s.absmax2.to(dev), s.dtype) for s in per_rank[0]], 0.0
     import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return [QuantStats(s.m, s.n, s.absmax.to(dev), s.absmax2.to(dev), s.dtype) for s in per_rank[0]], 0.0
 
     dist.barrier()
     sync()
@@ -623,8 +699,8 @@ def c5_section(args, rank, world, dev, dt, code, cpu):
     if not cpu:
         torch.cuda.synchronize()
     verified = wl.sanity(args.dtype) if mats else True
-    my_ms, _mode = time_steps(args, wl, dev, world, graph_ok=False)
-    t_ms, per = gather_times(my_ms, dev, world)
+    my_times, _mode = time_steps(args, wl, dev, world, graph_ok=False)
+    t_ms, per, _maxima = median_region(my_times, dev, world)
     els = W.C5_MATRICES * m * n
     alg = W.C5_MATRICES * algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256)
     per_rank = rank_figures(all_mats, per, args.steps)
@@ -721,7 +797,13 @@ def main():
         local_dev = local if dist_backend == "nccl" else local % max(1, ndev)
         torch.cuda.set_device(local_dev)
         dev = torch.device("cuda", local_dev)
-    if world > 1:
+    if world > 1 or args.dist_backend:
+        # an explicit --dist-backend at N = 1 still forms the (one-rank) group, so the
+        # RCCL scatter of the quant statistics runs on one GPU too
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -748,9 +830,9 @@ def main():
         torch.cuda.synchronize()
     wl.sanity(args.dtype)
 
-    # ---- timed region -------------------------------------------------------------------------
-    my_ms, launch_mode = time_steps(args, wl, dev, world)
-    t_ms, per_rank_ms = gather_times(my_ms, dev, world)
+    # ---- timed regions: R repeats of exactly K steps, the median region is the result ---------
+    my_times, launch_mode = time_steps(args, wl, dev, world)
+    t_ms, per_rank_ms, maxima = median_region(my_times, dev, world)
 
     # ---- figures -------------------------------------------------------------------------------
     my_alg = wl.alg_bytes()
@@ -759,31 +841,24 @@ def main():
     all_alg = sum(algorithmic_bytes(m, n, 2, m * n // 64, (m * n // 64 + 255) // 256)
                   for r in range(world) for _, m, n in all_mats[r])
     value = all_elems * args.steps / (t_ms * 1e-3)
-    kt_mean = my_ms * 1e3 / (args.steps * launches_per_step)  # us per launch, this rank
+    my_ms = per_rank_ms[rank]  # this rank's time in the median region
+    kt = my_ms * 1e3 / (args.steps * launches_per_step)  # us per launch, this rank
+    kts = sorted(t * 1e3 / (args.steps * launches_per_step) for t in my_times)
     m0, n0 = mats[0][1], mats[0][2]
     traffic, traffic_src = (None, None)
     if not cpu and len(mats) == 1:
         traffic, traffic_src = find_traffic(m0, n0, args.dtype)
-    achieved = my_alg / launches_per_step / (kt_mean * 1e-6)
+    achieved = my_alg / launches_per_step / (kt * 1e-6)
     regime = wl.regime()
     del wl
     if not cpu:
         torch.cuda.empty_cache()
-    # ---- the cache-warm figure (reported, never `value`): the round-1..3 rotation, 13
-    # full sets, whose 112 MB of packed weights stay in the Infinity Cache at 4096^2 ----------
-    cache_warm = None
-    if not cpu and not args.no_cache_warm and args.workload == "c2" and not (args.sets or args.in_sets):
-        wc = Workload(args, mats, stats, dev, dt, code, cfg_p, cpu, pin=CACHE_WARM_SETS, pout=CACHE_WARM_SETS)
-        cw_ms, _ = time_steps(args, wc, dev, world)
-        cw_t, _ = gather_times(cw_ms, dev, world)
-        cw_us = cw_ms * 1e3 / args.steps
-        cache_warm = {"ms_per_step": cw_t / args.steps, "launch_us_mean": cw_us,
-                      "frac": my_alg / (cw_us * 1e-6) / PEAK_HBM,
-                      "elements_per_s": all_elems * args.steps / (cw_t * 1e-3), **wc.regime(),
-                      "note": "packed weights re-read from the 256 MiB Infinity Cache (distinct reads < 256 MiB): "
-                              "not what a streamed model sees; round 1-3 headline regime"}
-        del wc
-        torch.cuda.empty_cache()
+    # ---- the memory-system twin (reported, never `value`): the same loads and stores
+    # with no decode, timed the same way on the same rotation -- the ceiling of this
+    # launch's access pattern (tools/stream_probe.hip twin_mix) --------------------------------
+    ceiling = None
+    if not cpu and not args.no_ceiling and len(mats) == 1 and args.launch == "eager":
+        ceiling = twin_ceiling(args, mats[0], dev, world, rank, my_alg, kt)
     if args.workload == "c5":
         metric = "dequantized elements/s (8 x 8192x8192 NF4->bf16, one matrix per GPU at N=8)"
         workload = (f"c5: 8 independent 8192x8192 NF4->{args.dtype} matrices (BASELINE configs[4]) split "
@@ -817,7 +892,7 @@ def main():
             "tile_dwords": args.tile_dwords, "blocks_per_cu": args.blocks_per_cu, "nontemporal": args.nontemporal,
             "flags": args.flags, "parallelism": f"shard{world} (independent matrices)",
             "cache_flush_before_timing": bool(not cpu and args.flush), "lead": args.lead,
-            "quant_state_scatter_ms": round(scatter_ms, 3), "dist_backend": dist_backend if world > 1 else None,
+            "quant_state_scatter_ms": round(scatter_ms, 3), "dist_backend": dist_backend if dist.is_initialized() else None,
         },
         "roofline": None if cpu else {
             "bound": "hbm",
@@ -828,11 +903,18 @@ def main():
             "traffic": traffic,
             "traffic_source": traffic_src,
             "kernel": "nf4_flat_kernel",
-            "launch_us_mean": kt_mean,
-            "launch_us_source": "HIP events over the timed region on the launch stream / launches (gaps included)",
+            "launch_us": kt,
+            "launch_us_min": kts[0],
+            "launch_us_median": kts[(len(kts) - 1) // 2],
+            "launch_us_max": kts[-1],
+            "launch_us_source": (f"HIP events on the launch stream over each of {len(my_times)} timed regions of "
+                                 f"{args.steps} steps (gaps included) / launches; the region with the median "
+                                 f"max-over-ranks time is the result"),
             "algorithmic_bytes_per_launch": my_alg // launches_per_step,
+            "ceiling_measured": ceiling,
         },
-        "cache_warm": cache_warm,
+        "repeats": {"regions": len(maxima), "steps_per_region": args.steps,
+                    "ms_per_step_by_region": [t / args.steps for t in maxima]},
         "cpu_baseline": None,
         "c5": None,
     }
@@ -847,7 +929,7 @@ def main():
             res["c5"]["cpu_baseline"] = c5_cpu_figures(args, code, threads)
     if rank == 0:
         print(json.dumps(res), file=result_out, flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

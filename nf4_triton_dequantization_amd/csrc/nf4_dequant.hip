@@ -132,6 +132,25 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_SCALE_NT
 #define NF4_DQ_SCALE_NT 0
 #endif
+//   NF4_DQ_DECODE       16-bit outputs: 1 (product) = per-block table of the 16 rounded
+//                       outputs in LDS, built by the block's 8 lanes (2 products + 1 rounding
+//                       each), then one 16-bit lookup per nibble whose LDS address is one
+//                       v_perm_b32; 0 = code lookup per nibble + fp32 multiply + rounding per
+//                       output (rounds 1-4; fp32 output always takes this path).  Round 5,
+//                       HBM-streamed 4096^2 bf16: 7.33-7.36 us per launch vs 7.62-7.65
+//                       (profiles/r05/dequant_decode_ab.jsonl)
+#ifndef NF4_DQ_DECODE
+#define NF4_DQ_DECODE 1
+#endif
+//   NF4_DQ_STORE_DELAY  > 0: s_sleep(n) (64 n clocks) once a tile's packed loads have arrived,
+//                       before its stores (table decode only)
+#ifndef NF4_DQ_STORE_DELAY
+#define NF4_DQ_STORE_DELAY 0
+#endif
+//   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
+#ifndef NF4_DQ_ABL_NOSCALE
+#define NF4_DQ_ABL_NOSCALE 0
+#endif
 
 constexpr int kWg = 256;   // rows / bitsandbytes-bytes kernels: 4 waves per workgroup
 constexpr int kFlatWaves = NF4_DQ_FLAT_WAVES;  // the flat kernel's workgroup
@@ -199,7 +218,10 @@ __device__ __forceinline__ TileIn tile_load(const Desc& D, __amdgpu_buffer_rsrc_
     };
     if constexpr (!NF4_DQ_SCALE_FIRST) packed_loads();
     const uint32_t g = tile_block<DT>(D, base, lane);
-    if constexpr (MODE == kRef) {
+    if constexpr (NF4_DQ_ABL_NOSCALE) {
+        in.a1 = g & 255u;
+        in.a2 = 0.01f;
+    } else if constexpr (MODE == kRef) {
         const uint32_t r = fdiv(g, D.bpr);
         const uint32_t b = g - r * D.bpr.d;
         const uint8_t* pa1 = D.a1 + fmodu(g, D.nb);
@@ -270,6 +292,65 @@ __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_
     }
 }
 
+// Stage 2, table decode (NF4_DQ_DECODE == 1, 16-bit outputs).  Dword j of lane l lies
+// in block 8j + l/8 of the tile, shared by the 8 lanes of group l/8; lane 8g + k rounds
+// the block's outputs for codes 2k and 2k+1 (the same fp32 products and RNE as the
+// per-nibble path) into dword k of the group's 16-entry table, at LDS byte tb + 4k
+// (tb = the wave's region + 256 g: byte 0 of tb is zero).  An output is then the 16-bit
+// entry at tb + 2 * code, and 2 * code is a byte of (w >> 3) & 0x1E1E1E1E (high nibbles)
+// or (w << 1) & 0x1E1E1E1E (low nibbles): v_perm_b32 moves that byte into tb's byte 0,
+// one instruction per address.  The 8 lanes of a group write their table before any of
+// them reads it in program order, and a wave's LDS accesses complete in order, so no
+// barrier; the next dword's table reuses the region after this one's reads.
+typedef uint16_t __attribute__((may_alias)) u16_alias;  // table entries are written as dwords
+typedef uint32_t __attribute__((may_alias)) u32_alias;
+
+struct TblCtx {
+    char* tbl;    // LDS base of the workgroup's tables
+    uint32_t tb;  // this lane's group table offset (multiple of 256)
+    f32x2 c01;    // NF4 codes 2k, 2k+1 of this lane (k = lane & 7)
+};
+
+template <int DT, int MODE>
+__device__ __forceinline__ void tile_finish_tbl(const Desc& D, __amdgpu_buffer_rsrc_t ro, const TileIn& in,
+                                                uint32_t base, uint32_t lane, const float* code2s,
+                                                const TblCtx& c) {
+    float s;
+    if constexpr (MODE == kRef) {
+        s = ((float)in.a1 / 127.0f) * in.a2;  // IEEE division (:45, :270), then fp32 multiply
+    } else if constexpr (MODE == kBnb) {
+        s = code2s[in.a1] * in.a2 + D.offset;
+    } else {
+        s = in.a2;
+    }
+    const uint32_t bsh = D.blk_shift;
+    const uint32_t k = lane & 7u;
+    if constexpr (NF4_DQ_STORE_DELAY > 0) {
+        // the loaded dwords as operands: the wait for them precedes the sleep
+        asm volatile("s_sleep %0" ::"i"(NF4_DQ_STORE_DELAY), "v"(in.w[0]), "v"(in.w[kU - 1]));
+    }
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+        const uint32_t rel = 256u * j + 4u * lane;
+        const float sj = __shfl(s, (int)(rel >> bsh), 64);
+        *reinterpret_cast<u32_alias*>(c.tbl + c.tb + 4u * k) = pack2<DT>(c.c01.x * sj, c.c01.y * sj);
+        const uint32_t w = in.w[j];
+        const uint32_t hb = (w >> 3) & 0x1E1E1E1Eu;
+        const uint32_t lb = (w << 1) & 0x1E1E1E1Eu;
+        uint32_t o[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t ah = __builtin_amdgcn_perm(hb, c.tb, 0x03020104u + b);
+            const uint32_t al = __builtin_amdgcn_perm(lb, c.tb, 0x03020104u + b);
+            const uint32_t vh = *reinterpret_cast<const u16_alias*>(c.tbl + ah);
+            const uint32_t vl = *reinterpret_cast<const u16_alias*>(c.tbl + al);
+            o[b] = vh | (vl << 16);
+        }
+        const u32x4 ov = {o[0], o[1], o[2], o[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(ov, ro, (base + rel) * 4u, 0, kAuxStore);
+    }
+}
+
 template <int MAXB>
 __device__ __forceinline__ uint32_t find_matrix(const Batch<MAXB>& bt, uint32_t t, uint32_t k) {
     if constexpr (MAXB > 1) {
@@ -314,6 +395,8 @@ template <int DT, int MODE, int MAXB>
 __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
     __shared__ __attribute__((aligned(16))) float lut[16];
     __shared__ __attribute__((aligned(16))) float code2s[MODE == kBnb ? 256 : 1];  // bitsandbytes code (every piece's)
+    constexpr bool kTbl = NF4_DQ_DECODE == 1 && DT != NF4DQ_F32;
+    __shared__ __attribute__((aligned(256))) char tbl[kTbl ? kFlatWaves * 2048 : 4];  // 8 block tables per wave
     const uint32_t lane = threadIdx.x & 63u;
 #if NF4_FLAT_STAMPS
     const unsigned long long t_entry = NF4_FNOW();
@@ -342,6 +425,12 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
         for (uint32_t i = threadIdx.x; i < 256u; i += kFlatWg) code2s[i] = bt.d[0].code2[i];
     }
     __syncthreads();
+    TblCtx tc{};
+    if constexpr (kTbl) {
+        tc.tbl = tbl;
+        tc.tb = ((threadIdx.x >> 6) << 11) + ((lane >> 3) << 8);
+        tc.c01 = *reinterpret_cast<const f32x2*>(lut + 2u * (lane & 7u));
+    }
     if (!ca.valid) {
         NF4_FSTAMP(0, t_entry);
         NF4_FSTAMP(1, 0ull);
@@ -354,7 +443,8 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
         __amdgpu_buffer_rsrc_t rpb = rpa, rob = roa;
         if (MAXB > 1 && cb.k != ca.k) make_rsrcs<DT>(bt, cb.k, rpb, rob);
         TileIn B = tile_load<DT, MODE>(bt.d[cb.k], rpb, cb.base, lane);
-        tile_finish<DT, MODE>(bt.d[ca.k], roa, lut, A, ca.base, lane, code2s);
+        if constexpr (kTbl) tile_finish_tbl<DT, MODE>(bt.d[ca.k], roa, A, ca.base, lane, code2s, tc);
+        else tile_finish<DT, MODE>(bt.d[ca.k], roa, lut, A, ca.base, lane, code2s);
 #if NF4_FLAT_STAMPS
         if (tiles_done == 0) NF4_FSTAMP(1, NF4_FNOW());
         ++tiles_done;
@@ -365,7 +455,8 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
         __amdgpu_buffer_rsrc_t rpn = rpb, ron = rob;
         if (MAXB > 1 && cn.k != cb.k) make_rsrcs<DT>(bt, cn.k, rpn, ron);
         A = tile_load<DT, MODE>(bt.d[cn.k], rpn, cn.base, lane);
-        tile_finish<DT, MODE>(bt.d[cb.k], rob, lut, B, cb.base, lane, code2s);
+        if constexpr (kTbl) tile_finish_tbl<DT, MODE>(bt.d[cb.k], rob, B, cb.base, lane, code2s, tc);
+        else tile_finish<DT, MODE>(bt.d[cb.k], rob, lut, B, cb.base, lane, code2s);
 #if NF4_FLAT_STAMPS
         ++tiles_done;
 #endif

@@ -11,6 +11,9 @@
 //   DQV_ST=p   cache-policy bits of the output stores (product 18 = sc1 + nt)
 //   DQV_SF=1   a tile's scale loads issued before its packed loads
 //   DQV_SNT=1  the absmax / nested-scale gathers with the nt policy
+//   DQV_NOSCALE=1  ablation: no scale loads (wrong results; timing only)
+//   DQV_DELAY=n    s_sleep(n) between a tile's loads arriving and its stores (table decode)
+//   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
 #endif
@@ -28,6 +31,16 @@
 #endif
 #ifdef DQV_SNT
 #define NF4_DQ_SCALE_NT DQV_SNT
+#endif
+
+#ifdef DQV_NOSCALE
+#define NF4_DQ_ABL_NOSCALE DQV_NOSCALE
+#endif
+#ifdef DQV_DELAY
+#define NF4_DQ_STORE_DELAY DQV_DELAY
+#endif
+#ifdef DQV_DEC
+#define NF4_DQ_DECODE DQV_DEC
 #endif
 
 #include "../nf4_triton_dequantization_amd/csrc/nf4_dequant.hip"
