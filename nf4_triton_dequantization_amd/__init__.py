@@ -15,6 +15,7 @@ from .kernel import (  # noqa: F401
     dequantize_nf4_many,
     nf4_linear,
     nf4_linear_grouped,
+    release_gemm_workspaces,
     reset_triton_dequantize_state,
     triton_dequantize_nf4,
 )
@@ -22,6 +23,7 @@ from .bnb_layout import Linear4bit, Params4bit, QuantState, quantize_nf4  # noqa
 from .checkpoint import load_nf4_safetensors, save_nf4_safetensors  # noqa: F401
 
 __all__ = ["triton_dequantize_nf4", "reset_triton_dequantize_state", "dequantize_nf4_many",
-           "dequantize_nf4_bnb", "dequantize_nf4_into", "nf4_linear", "nf4_linear_grouped", "check_gemm_workspaces", "Linear4bit",
+           "dequantize_nf4_bnb", "dequantize_nf4_into", "nf4_linear", "nf4_linear_grouped", "check_gemm_workspaces",
+           "release_gemm_workspaces", "Linear4bit",
            "Params4bit", "QuantState", "quantize_nf4", "load_nf4_safetensors", "save_nf4_safetensors"]
 __version__ = "0.1.0"

@@ -147,6 +147,14 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_STORE_DELAY
 #define NF4_DQ_STORE_DELAY 0
 #endif
+//   NF4_DQ_A1_AUX / NF4_DQ_A2_AUX  >= 0: the reference-mode absmax byte / nested-absmax
+//                       gathers as buffer loads with these cache-policy bits (-1: plain loads)
+#ifndef NF4_DQ_A1_AUX
+#define NF4_DQ_A1_AUX -1
+#endif
+#ifndef NF4_DQ_A2_AUX
+#define NF4_DQ_A2_AUX -1
+#endif
 //   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
@@ -226,7 +234,20 @@ __device__ __forceinline__ TileIn tile_load(const Desc& D, __amdgpu_buffer_rsrc_
         const uint32_t b = g - r * D.bpr.d;
         const uint8_t* pa1 = D.a1 + fmodu(g, D.nb);
         const float* pa2 = D.a2 + fmodu(r * D.groups + (b >> 2), D.n2);
-        if constexpr (NF4_DQ_SCALE_NT) {
+        if constexpr (NF4_DQ_A1_AUX >= 0 || NF4_DQ_A2_AUX >= 0) {
+            if constexpr (NF4_DQ_A1_AUX >= 0) {
+                const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc((void*)D.a1, 0, 0x7FFFFFFF, kRsrcFlags);
+                in.a1 = __builtin_amdgcn_raw_buffer_load_b8(r1, (uint32_t)(pa1 - D.a1), 0, NF4_DQ_A1_AUX);
+            } else {
+                in.a1 = *pa1;
+            }
+            if constexpr (NF4_DQ_A2_AUX >= 0) {
+                const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc((void*)D.a2, 0, 0x7FFFFFFF, kRsrcFlags);
+                in.a2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2, (uint32_t)(pa2 - D.a2) * 4u, 0, NF4_DQ_A2_AUX));
+            } else {
+                in.a2 = *pa2;
+            }
+        } else if constexpr (NF4_DQ_SCALE_NT) {
             in.a1 = __builtin_nontemporal_load(pa1);
             in.a2 = __builtin_nontemporal_load(pa2);
         } else {

@@ -138,6 +138,10 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 // missing partials read as NaN AND the workspace's sticky error word (kErrWord,
 // after the counters) is set, so the host learns of it (nf4_gemm_check_workspace)
 // instead of finding NaNs nobody reported -- never a hung GPU, never a silent one.
+// The word also poisons later calls on the same workspace: a slice that timed out
+// may still store its partial after the reducer cleared the entry, and a later call
+// would read that stale entry as written; so while the word is set every reducer
+// writes NaN instead of its sum, until the host's check re-zeroes the workspace.
 constexpr int kSpinMax = 1 << 16;
 constexpr uint32_t kErrWord = 16384;  // uint32 index in the workspace header (byte 64 KiB)
 
@@ -223,6 +227,8 @@ __device__ __forceinline__ void splitk_reduce(uint64_t* slab, uint32_t ksplit, u
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     const uint32_t total = M * KP;
     const uint32_t sstride = M * (ncols >> 1);  // entries per slice
+    // a workspace whose error word is set may hold stale entries: report, never sum them
+    const bool poisoned = __hip_atomic_load(counters + kErrWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     for (uint32_t base = 0; base < total; base += 64u * kU) {
         float s0[kU], s1[kU];
         uint32_t idx[kU];
@@ -267,7 +273,7 @@ __device__ __forceinline__ void splitk_reduce(uint64_t* slab, uint32_t ksplit, u
             if (e < total) {
                 uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(y) + (e / KP) * yld + ycol0 +
                                                             2u * (e % KP));
-                *dst = pack2<DT>(s0[u], s1[u]);
+                *dst = poisoned ? pack2<DT>(__builtin_nanf(""), __builtin_nanf("")) : pack2<DT>(s0[u], s1[u]);
             }
         }
     }

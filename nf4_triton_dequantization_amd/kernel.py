@@ -395,6 +395,11 @@ def _launch_bnb(q, qs, out, code, numel, bs) -> int:
     return rc
 
 
+# (device index, raw stream handle) -> (workspace, the torch stream object): holding the
+# stream object keeps a torch-created stream alive for the cache's lifetime, so the
+# check below never hands HIP a dangling handle (an ExternalStream's owner must keep
+# its stream alive while nf4_linear has a workspace for it, or call
+# release_gemm_workspaces() first)
 _GEMM_WS = {}
 
 
@@ -413,12 +418,23 @@ def _gemm_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     buffer stays valid; a new stream gets its own (calls on different streams
     may run concurrently and must not share counters).
     """
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
-    ws = _GEMM_WS.get(key)
+    stream = torch.cuda.current_stream(device)
+    key = (device.index, stream.cuda_stream)
+    ent = _GEMM_WS.get(key)
+    ws = ent[0] if ent is not None else None
     if ws is None or ws.numel() < nbytes:
         ws = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
-        _GEMM_WS[key] = ws
+        _GEMM_WS[key] = (ws, stream)
     return ws
+
+
+def release_gemm_workspaces() -> None:
+    """Forget every cached split-K workspace (after a synchronize of their streams):
+    for callers that destroy their own external streams."""
+    for (dev_index, _), (ws, stream) in list(_GEMM_WS.items()):
+        with torch.cuda.device(dev_index):
+            stream.synchronize()
+    _GEMM_WS.clear()
 
 
 def check_gemm_workspaces() -> None:
@@ -432,10 +448,11 @@ def check_gemm_workspaces() -> None:
     """
     bad = []
     L = _lib.lib() if _GEMM_WS else None
-    for (dev_index, stream), ws in list(_GEMM_WS.items()):
-        rc = L.nf4_gemm_check_workspace(ws.data_ptr(), ws.numel(), stream)
+    for (dev_index, handle), (ws, stream) in list(_GEMM_WS.items()):
+        with torch.cuda.device(dev_index):  # the HIP calls run on the workspace's device
+            rc = L.nf4_gemm_check_workspace(ws.data_ptr(), ws.numel(), stream.cuda_stream)
         if rc:
-            bad.append(f"cuda:{dev_index} stream {stream:#x}: {_lib.strerror(rc)}")
+            bad.append(f"cuda:{dev_index} stream {handle:#x}: {_lib.strerror(rc)}")
     if bad:
         raise RuntimeError("nf4 fused GEMM: " + "; ".join(bad))
 

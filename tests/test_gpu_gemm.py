@@ -868,3 +868,90 @@ def test_balanced_kernel_rejects_what_it_cannot_spread(gpu):
         rc = L.nf4_gemm_ref_cfg(F, M, F, N * K // 2, F, N * K // 64, F, 16, F, _lib.BF16, N, K, F, 1 << 30,
                                 ctypes.byref(c), None)
         assert rc in (_lib.ERR_ARG, _lib.ERR_SHAPE), (M, N, K, rc)
+
+
+def _splitk3_cfg(L, _lib, x, t, y, N, K):
+    """A persistent-kernel configuration with more than two K slices (ticket + poll
+    hand-off, splitk_reduce; two slices would take the exchange) that the library
+    accepts for this shape."""
+    for ks in (4, 3, 8):
+        for waves in (4, 8, 16):
+            for depth in (1, 2, 4, 8):
+                for strips in (1, 2, 4):
+                    cfg = _lib.GemmCfg(_lib.GEMM_PERSIST, waves, depth, ks, strips)
+                    if _gemm_cfg_call(L, _lib, x, t, y, _lib.BF16, N, K, cfg) == 0:
+                        return cfg
+    raise AssertionError("no persistent configuration with > 2 K slices accepted")
+
+
+def test_splitk_error_word_is_reported_and_poisons_later_calls(coracle, gpu):
+    """the split-K error path.  A set error word (what a reducer that gave
+    up waiting leaves) is reported by nf4_gemm_check_workspace as ERR_SPLITK_TIMEOUT and
+    the workspace comes back zeroed; while it is set, every split-K reducer writes NaN
+    instead of a sum (a timed-out slice's late store could otherwise pass for a
+    written partial in a later call); after the check the next call is exact again."""
+    import ctypes
+
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    M, N, K = 4, 256, 4096
+    packed, a1, a2 = O.make_inputs(N, K, seed=4242, a2_kind="normal")
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16)
+    t = (torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu))
+    xt, xb = _x_bits(M, K, "bf16", seed=31)
+    x = xt.to(gpu)
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=gpu)
+    cfg = _splitk3_cfg(L, _lib, x, t, y, N, K)
+    wsz = L.nf4_gemm_workspace_bytes_cfg(M, N, K, ctypes.byref(cfg))
+    assert wsz >= 65536 + 4
+    ws = torch.zeros(wsz, dtype=torch.uint8, device=gpu)
+    sp = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        y.fill_(0.0)
+        rc = L.nf4_gemm_ref_cfg(x.data_ptr(), M, t[0].data_ptr(), t[0].numel(), t[1].data_ptr(), t[1].numel(),
+                                t[2].data_ptr(), t[2].numel(), y.data_ptr(), _lib.BF16, N, K, ws.data_ptr(), wsz,
+                                ctypes.byref(cfg), sp)
+        torch.cuda.synchronize()
+        assert rc == 0, _lib.strerror(rc)
+
+    run()
+    _check(y, xb, W, "bf16")
+    assert L.nf4_gemm_check_workspace(ws.data_ptr(), wsz, sp) == _lib.OK
+    # 1. reported, and the workspace is re-zeroed
+    ws[65536] = 1
+    assert L.nf4_gemm_check_workspace(ws.data_ptr(), wsz, sp) == _lib.ERR_SPLITK_TIMEOUT
+    assert int(ws.count_nonzero()) == 0
+    assert L.nf4_gemm_check_workspace(ws.data_ptr(), wsz, sp) == _lib.OK
+    # 2. a set word poisons the next calls: NaN, never a sum of possibly stale partials
+    ws[65536] = 1
+    run()
+    assert bool(torch.isnan(y.float()).all())
+    run()
+    assert bool(torch.isnan(y.float()).all())
+    assert L.nf4_gemm_check_workspace(ws.data_ptr(), wsz, sp) == _lib.ERR_SPLITK_TIMEOUT
+    run()
+    _check(y, xb, W, "bf16")
+    assert L.nf4_gemm_check_workspace(ws.data_ptr(), wsz, sp) == _lib.OK
+
+
+def test_check_gemm_workspaces_raises_on_a_set_error_word(coracle, gpu):
+    """check_gemm_workspaces() raises RuntimeError naming the stream when a cached
+    workspace's error word is set, and is clean on the next check (the library zeroed it)."""
+    from nf4_triton_dequantization_amd import check_gemm_workspaces, kernel, nf4_linear
+
+    M, N, K = 16, 4096, 4096  # the persistent kernel's K slices: a cached workspace
+    packed, a1, a2 = O.make_inputs(N, K, seed=77)
+    mod = make_module(packed, a1, a2, N, K, "bf16", gpu)
+    xt, _ = _x_bits(M, K, "bf16", seed=3)
+    nf4_linear(xt.to(gpu), mod)
+    torch.cuda.synchronize()
+    key = (gpu.index if gpu.index is not None else 0, torch.cuda.current_stream(gpu).cuda_stream)
+    assert key in kernel._GEMM_WS
+    ws, _stream = kernel._GEMM_WS[key]
+    assert check_gemm_workspaces() is None
+    ws[65536] = 1
+    with pytest.raises(RuntimeError, match="split-K"):
+        check_gemm_workspaces()
+    assert check_gemm_workspaces() is None

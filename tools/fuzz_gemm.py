@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--seconds", type=float, default=500.0)
     ap.add_argument("--cfg-rate", type=float, default=0.25, help="share of cases that also run a drawn configuration")
+    ap.add_argument("--boundary-rate", type=float, default=0.1,
+                    help="share of cases drawn from the default-rule boundary shapes (large N, K = 14336)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     L = _lib.lib()
@@ -83,6 +85,13 @@ def main():
         M = int(rng.integers(1, 33))
         N = 64 * int(rng.integers(1, 49))
         K = 128 * int(rng.integers(1, 49))
+        if rng.random() < args.boundary_rate:
+            # the default-rule boundaries the uniform draw cannot reach: M on
+            # either side of 8 / 16 / 24, the wide launches (16-wave whole-K XR at
+            # N >= 24576, persistent strips = 4 at N >= 8192) and the down projection's K
+            M = int(rng.choice([1, 8, 9, 16, 17, 24, 25, 32]))
+            N, K = [(1024, 4096), (4096, 4096), (8192, 4096), (14336, 4096), (24576, 4096), (28672, 4096),
+                    (4096, 14336), (1024, 14336)][int(rng.integers(0, 8))]
         dt = "bf16" if rng.random() < 0.6 else "f16"
         nb_full = N * K // 64
         ov = {"a2_kind": "normal" if rng.random() < 0.5 else "uniform"}
