@@ -298,8 +298,8 @@ def cpu_baseline(shapes, seconds, dtype_code):
 
 
 def find_traffic(m, n, dtype):
-    for rnd in ROUNDS:
-        path = os.path.join(REPO, "profiles", rnd, "pmc_traffic.json")
+    for rnd, name in [(r, f) for r in ROUNDS for f in ("pmc_traffic.json", f"pmc_traffic_{dtype}.json")]:
+        path = os.path.join(REPO, "profiles", rnd, name)
         if not os.path.exists(path):
             continue
         try:
@@ -308,7 +308,7 @@ def find_traffic(m, n, dtype):
         except (OSError, ValueError):
             continue
         if pmc.get("m") == m and pmc.get("n") == n and pmc.get("dtype") == dtype:
-            return pmc.get("hbm_bytes_per_launch"), f"profiles/{rnd}/pmc_traffic.json"
+            return pmc.get("hbm_bytes_per_launch"), f"profiles/{rnd}/{name}"
     return None, None
 
 

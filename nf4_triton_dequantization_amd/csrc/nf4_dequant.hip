@@ -155,6 +155,11 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_A2_AUX
 #define NF4_DQ_A2_AUX -1
 #endif
+//   NF4_DQ_TBL_NOLUT    1: the table decode takes its two codes per lane from immediates, so
+//                       the kernel writes no LDS code table and has no barrier
+#ifndef NF4_DQ_TBL_NOLUT
+#define NF4_DQ_TBL_NOLUT 0
+#endif
 //   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
@@ -441,16 +446,25 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
 #pragma unroll
         for (int j = 0; j < kU; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, roa, 0xFFFFF000u + 16u * j, 0, kAuxStore);
     }
-    write_lut(lut);
-    if constexpr (MODE == kBnb) {  // every piece of a bitsandbytes stream carries the same code
-        for (uint32_t i = threadIdx.x; i < 256u; i += kFlatWg) code2s[i] = bt.d[0].code2[i];
+    // the table decode shares nothing between the waves of a workgroup (each wave owns
+    // its tables; a lane's two codes come from immediates): no LDS code table, no barrier
+    constexpr bool kNoLut = kTbl && NF4_DQ_TBL_NOLUT && MODE != kBnb;
+    if constexpr (!kNoLut) {
+        write_lut(lut);
+        if constexpr (MODE == kBnb) {  // every piece of a bitsandbytes stream carries the same code
+            for (uint32_t i = threadIdx.x; i < 256u; i += kFlatWg) code2s[i] = bt.d[0].code2[i];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     TblCtx tc{};
     if constexpr (kTbl) {
         tc.tbl = tbl;
         tc.tb = ((threadIdx.x >> 6) << 11) + ((lane >> 3) << 8);
-        tc.c01 = *reinterpret_cast<const f32x2*>(lut + 2u * (lane & 7u));
+        if constexpr (kNoLut) {
+            tc.c01 = f32x2{nf4_code(2u * (lane & 7u)), nf4_code(2u * (lane & 7u) + 1u)};
+        } else {
+            tc.c01 = *reinterpret_cast<const f32x2*>(lut + 2u * (lane & 7u));
+        }
     }
     if (!ca.valid) {
         NF4_FSTAMP(0, t_entry);

@@ -5,7 +5,8 @@
    two access shapes;
 2. the bench workload: 4096x4096 NF4->bf16 dequant, bench.py's rotation (round 4:
    input and output sets rotated independently, >= 512 MiB of distinct reads and of
-   writes, so the weights stream from HBM), 96 launches of the product entry.
+   writes, so the weights stream from HBM), 96 launches of the product entry; output
+   dtype PMC_DTYPE (bf16, default, or f16).
 """
 import ctypes
 import os
@@ -47,12 +48,13 @@ def main():
     ins = [(torch.randint(0, 256, (m * n // 2,), dtype=torch.uint8, device=dev, generator=g),
             torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=g),
             torch.rand(n2, device=dev, generator=g) * 0.01) for _ in range(pin)]
-    outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(pout)]
+    f16 = os.environ.get("PMC_DTYPE", "bf16") == "f16"  # BASELINE configs[3]: the fp16 leg
+    outs = [torch.empty((m, n), dtype=torch.float16 if f16 else torch.bfloat16, device=dev) for _ in range(pout)]
     L = _lib.lib()
     for i in range(96):
         q, a1, a2 = ins[i % pin]
         assert L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
-                                 outs[i % pout].data_ptr(), _lib.BF16, m, n, st) == 0
+                                 outs[i % pout].data_ptr(), _lib.F16 if f16 else _lib.BF16, m, n, st) == 0
     torch.cuda.synchronize()
     print("pmc probe done", m, n)
 

@@ -58,7 +58,7 @@ def main():
     N = m * n
     alg_r = N // 2 + N // 64 + 4 * ((N // 64 + 255) // 256)
     alg_w = 2 * N
-    res = {"m": m, "n": n, "dtype": "bf16",
+    res = {"m": m, "n": n, "dtype": os.environ.get("PMC_DTYPE", "bf16"),
            "fetch_kib_raw": kf, "write_kib_raw": kw, "dispatches": [nf, nw],
            "read_factor_dword_loads": rf, "write_factor_x4_nt_stores": wf,
            "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,

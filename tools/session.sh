@@ -98,8 +98,8 @@ for stage in "$@"; do
         trace configs_c5 nf4_flat_kernel 32 600 -- tools/bench_configs.py --configs c5
         trace bench_8192 nf4_flat_kernel 64 300 -- bench.py --m 8192 --n 8192 --steps 64 --no-cpu-baseline ;;
     rocprof)
-        trace bench nf4_flat_kernel 200 300 -- bench.py --steps 200 --no-cpu-baseline --no-c5 --no-cache-warm \
-            --spin-us-per-launch 150
+        trace bench nf4_flat_kernel 200 300 -- bench.py --steps 200 --repeats 1 --no-cpu-baseline --no-c5 \
+            --no-ceiling --spin-us-per-launch 150
         python3 tools/rocprof_summary.py "$O/prof_bench" nf4_flat_kernel "$O/rocprof_bench_summary.json" \
             "$O/rocprof_bench_kernel_stats.csv" --last 200 > /dev/null ;;
     pmc)  # headline HBM traffic (FETCH_SIZE / WRITE_SIZE passes, calibrated) + decode-GEMM SQ counters
@@ -110,6 +110,14 @@ for stage in "$@"; do
             python3 -u tools/pmc_probe.py > "$O/pmc_write.log" 2>&1
         python3 tools/pmc_traffic.py "$O/pmc" "$O/pmc_traffic.json" > "$O/pmc_traffic.log" 2>&1
         cat "$O/pmc_traffic.json"
+        rm -rf "$O/pmc"
+        # the fp16 leg of BASELINE configs[3] (C4), same passes
+        PMC_DTYPE=f16 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc" -o fetch -- \
+            python3 -u tools/pmc_probe.py > "$O/pmc_fetch_f16.log" 2>&1
+        PMC_DTYPE=f16 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc" -o write -- \
+            python3 -u tools/pmc_probe.py > "$O/pmc_write_f16.log" 2>&1
+        PMC_DTYPE=f16 python3 tools/pmc_traffic.py "$O/pmc" "$O/pmc_traffic_f16.json" > "$O/pmc_traffic_f16.log" 2>&1
+        cat "$O/pmc_traffic_f16.json"
         GA="tools/gemm_ab.py --ms ${PMC_M:-32} --shapes ${PMC_SHAPE:-14336,4096} --budget-mb 512"
         timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
             SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM --output-format csv -d "$O/pmcg_a" -o a -- \
