@@ -160,6 +160,12 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_TBL_NOLUT
 #define NF4_DQ_TBL_NOLUT 0
 #endif
+//   NF4_DQ_SYNC_STORES  1: table decode holds a tile's 4 output dwords until a workgroup
+//                       barrier, so the workgroup's waves issue their stores together
+//                       (tools only: the barrier assumes equal tile counts per wave)
+#ifndef NF4_DQ_SYNC_STORES
+#define NF4_DQ_SYNC_STORES 0
+#endif
 //   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
@@ -351,6 +357,8 @@ __device__ __forceinline__ void tile_finish_tbl(const Desc& D, __amdgpu_buffer_r
     }
     const uint32_t bsh = D.blk_shift;
     const uint32_t k = lane & 7u;
+    u32x4 held[NF4_DQ_SYNC_STORES ? kU : 1];
+    (void)held;
     if constexpr (NF4_DQ_STORE_DELAY > 0) {
         // the loaded dwords as operands: the wait for them precedes the sleep
         asm volatile("s_sleep %0" ::"i"(NF4_DQ_STORE_DELAY), "v"(in.w[0]), "v"(in.w[kU - 1]));
@@ -373,7 +381,17 @@ __device__ __forceinline__ void tile_finish_tbl(const Desc& D, __amdgpu_buffer_r
             o[b] = vh | (vl << 16);
         }
         const u32x4 ov = {o[0], o[1], o[2], o[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(ov, ro, (base + rel) * 4u, 0, kAuxStore);
+        if constexpr (NF4_DQ_SYNC_STORES) {
+            held[j] = ov;
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b128(ov, ro, (base + rel) * 4u, 0, kAuxStore);
+        }
+    }
+    if constexpr (NF4_DQ_SYNC_STORES) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kU; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(held[j], ro, (base + 256u * j + 4u * lane) * 4u, 0, kAuxStore);
     }
 }
 

@@ -15,6 +15,7 @@
 //   DQV_DELAY=n    s_sleep(n) between a tile's loads arriving and its stores (table decode)
 //   DQV_A1=p / DQV_A2=p  absmax / nested-absmax gathers as buffer loads with policy p
 //   DQV_NOLUT=1    table decode without the LDS code table and its barrier
+//   DQV_SYNC=1     table decode: a workgroup barrier before each tile's stores
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
@@ -49,6 +50,9 @@
 #endif
 #ifdef DQV_NOLUT
 #define NF4_DQ_TBL_NOLUT DQV_NOLUT
+#endif
+#ifdef DQV_SYNC
+#define NF4_DQ_SYNC_STORES DQV_SYNC
 #endif
 #ifdef DQV_DEC
 #define NF4_DQ_DECODE DQV_DEC
