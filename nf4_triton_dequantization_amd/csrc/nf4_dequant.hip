@@ -142,30 +142,6 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_DECODE
 #define NF4_DQ_DECODE 1
 #endif
-//   NF4_DQ_STORE_DELAY  > 0: s_sleep(n) (64 n clocks) once a tile's packed loads have arrived,
-//                       before its stores (table decode only)
-#ifndef NF4_DQ_STORE_DELAY
-#define NF4_DQ_STORE_DELAY 0
-#endif
-//   NF4_DQ_A1_AUX / NF4_DQ_A2_AUX  >= 0: the reference-mode absmax byte / nested-absmax
-//                       gathers as buffer loads with these cache-policy bits (-1: plain loads)
-#ifndef NF4_DQ_A1_AUX
-#define NF4_DQ_A1_AUX -1
-#endif
-#ifndef NF4_DQ_A2_AUX
-#define NF4_DQ_A2_AUX -1
-#endif
-//   NF4_DQ_TBL_NOLUT    1: the table decode takes its two codes per lane from immediates, so
-//                       the kernel writes no LDS code table and has no barrier
-#ifndef NF4_DQ_TBL_NOLUT
-#define NF4_DQ_TBL_NOLUT 0
-#endif
-//   NF4_DQ_SYNC_STORES  1: table decode holds a tile's 4 output dwords until a workgroup
-//                       barrier, so the workgroup's waves issue their stores together
-//                       (tools only: the barrier assumes equal tile counts per wave)
-#ifndef NF4_DQ_SYNC_STORES
-#define NF4_DQ_SYNC_STORES 0
-#endif
 //   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
@@ -245,20 +221,7 @@ __device__ __forceinline__ TileIn tile_load(const Desc& D, __amdgpu_buffer_rsrc_
         const uint32_t b = g - r * D.bpr.d;
         const uint8_t* pa1 = D.a1 + fmodu(g, D.nb);
         const float* pa2 = D.a2 + fmodu(r * D.groups + (b >> 2), D.n2);
-        if constexpr (NF4_DQ_A1_AUX >= 0 || NF4_DQ_A2_AUX >= 0) {
-            if constexpr (NF4_DQ_A1_AUX >= 0) {
-                const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc((void*)D.a1, 0, 0x7FFFFFFF, kRsrcFlags);
-                in.a1 = __builtin_amdgcn_raw_buffer_load_b8(r1, (uint32_t)(pa1 - D.a1), 0, NF4_DQ_A1_AUX);
-            } else {
-                in.a1 = *pa1;
-            }
-            if constexpr (NF4_DQ_A2_AUX >= 0) {
-                const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc((void*)D.a2, 0, 0x7FFFFFFF, kRsrcFlags);
-                in.a2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2, (uint32_t)(pa2 - D.a2) * 4u, 0, NF4_DQ_A2_AUX));
-            } else {
-                in.a2 = *pa2;
-            }
-        } else if constexpr (NF4_DQ_SCALE_NT) {
+        if constexpr (NF4_DQ_SCALE_NT) {
             in.a1 = __builtin_nontemporal_load(pa1);
             in.a2 = __builtin_nontemporal_load(pa2);
         } else {
@@ -357,12 +320,6 @@ __device__ __forceinline__ void tile_finish_tbl(const Desc& D, __amdgpu_buffer_r
     }
     const uint32_t bsh = D.blk_shift;
     const uint32_t k = lane & 7u;
-    u32x4 held[NF4_DQ_SYNC_STORES ? kU : 1];
-    (void)held;
-    if constexpr (NF4_DQ_STORE_DELAY > 0) {
-        // the loaded dwords as operands: the wait for them precedes the sleep
-        asm volatile("s_sleep %0" ::"i"(NF4_DQ_STORE_DELAY), "v"(in.w[0]), "v"(in.w[kU - 1]));
-    }
 #pragma unroll
     for (int j = 0; j < kU; ++j) {
         const uint32_t rel = 256u * j + 4u * lane;
@@ -381,17 +338,7 @@ __device__ __forceinline__ void tile_finish_tbl(const Desc& D, __amdgpu_buffer_r
             o[b] = vh | (vl << 16);
         }
         const u32x4 ov = {o[0], o[1], o[2], o[3]};
-        if constexpr (NF4_DQ_SYNC_STORES) {
-            held[j] = ov;
-        } else {
-            __builtin_amdgcn_raw_buffer_store_b128(ov, ro, (base + rel) * 4u, 0, kAuxStore);
-        }
-    }
-    if constexpr (NF4_DQ_SYNC_STORES) {
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kU; ++j)
-            __builtin_amdgcn_raw_buffer_store_b128(held[j], ro, (base + 256u * j + 4u * lane) * 4u, 0, kAuxStore);
+        __builtin_amdgcn_raw_buffer_store_b128(ov, ro, (base + rel) * 4u, 0, kAuxStore);
     }
 }
 
@@ -464,25 +411,18 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
 #pragma unroll
         for (int j = 0; j < kU; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, roa, 0xFFFFF000u + 16u * j, 0, kAuxStore);
     }
-    // the table decode shares nothing between the waves of a workgroup (each wave owns
-    // its tables; a lane's two codes come from immediates): no LDS code table, no barrier
-    constexpr bool kNoLut = kTbl && NF4_DQ_TBL_NOLUT && MODE != kBnb;
-    if constexpr (!kNoLut) {
-        write_lut(lut);
-        if constexpr (MODE == kBnb) {  // every piece of a bitsandbytes stream carries the same code
-            for (uint32_t i = threadIdx.x; i < 256u; i += kFlatWg) code2s[i] = bt.d[0].code2[i];
-        }
-        __syncthreads();
+    // (the table decode could take its two codes from immediates and skip this table and
+    // the barrier: measured 8 % slower, profiles/r05/nolut_scalefirst_variants.jsonl)
+    write_lut(lut);
+    if constexpr (MODE == kBnb) {  // every piece of a bitsandbytes stream carries the same code
+        for (uint32_t i = threadIdx.x; i < 256u; i += kFlatWg) code2s[i] = bt.d[0].code2[i];
     }
+    __syncthreads();
     TblCtx tc{};
     if constexpr (kTbl) {
         tc.tbl = tbl;
         tc.tb = ((threadIdx.x >> 6) << 11) + ((lane >> 3) << 8);
-        if constexpr (kNoLut) {
-            tc.c01 = f32x2{nf4_code(2u * (lane & 7u)), nf4_code(2u * (lane & 7u) + 1u)};
-        } else {
-            tc.c01 = *reinterpret_cast<const f32x2*>(lut + 2u * (lane & 7u));
-        }
+        tc.c01 = *reinterpret_cast<const f32x2*>(lut + 2u * (lane & 7u));
     }
     if (!ca.valid) {
         NF4_FSTAMP(0, t_entry);

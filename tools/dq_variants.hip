@@ -12,10 +12,9 @@
 //   DQV_SF=1   a tile's scale loads issued before its packed loads
 //   DQV_SNT=1  the absmax / nested-scale gathers with the nt policy
 //   DQV_NOSCALE=1  ablation: no scale loads (wrong results; timing only)
-//   DQV_DELAY=n    s_sleep(n) between a tile's loads arriving and its stores (table decode)
-//   DQV_A1=p / DQV_A2=p  absmax / nested-absmax gathers as buffer loads with policy p
-//   DQV_NOLUT=1    table decode without the LDS code table and its barrier
-//   DQV_SYNC=1     table decode: a workgroup barrier before each tile's stores
+// Round 5 also measured store delays, scale-gather buffer loads / policies, a table decode
+// without the code table and its barrier, and synchronised stores through hooks removed
+// after measurement (profiles/r05/; the hooks are in git history at 914c6b8).
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
@@ -38,21 +37,6 @@
 
 #ifdef DQV_NOSCALE
 #define NF4_DQ_ABL_NOSCALE DQV_NOSCALE
-#endif
-#ifdef DQV_DELAY
-#define NF4_DQ_STORE_DELAY DQV_DELAY
-#endif
-#ifdef DQV_A1
-#define NF4_DQ_A1_AUX DQV_A1
-#endif
-#ifdef DQV_A2
-#define NF4_DQ_A2_AUX DQV_A2
-#endif
-#ifdef DQV_NOLUT
-#define NF4_DQ_TBL_NOLUT DQV_NOLUT
-#endif
-#ifdef DQV_SYNC
-#define NF4_DQ_SYNC_STORES DQV_SYNC
 #endif
 #ifdef DQV_DEC
 #define NF4_DQ_DECODE DQV_DEC
