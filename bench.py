@@ -18,7 +18,7 @@ NF4->bf16 (configs[1]).  A *step* is one pass of the hot path over one batch:
 before this process touches the GPU and relays rank 0's line; under a launcher
 WORLD_SIZE must equal N.
 
-Timed regions (``value``): R = ``--repeats`` (default 5) regions of exactly K steps,
+Timed regions (``value``): R = ``--repeats`` (default 7) regions of exactly K steps,
 each K eager launches of the product C-ABI entry (``nf4_dequant_ref``, arguments
 prepared up front), bracketed by barrier + synchronize on both sides, HIP events on the
 launch stream around them.  Per region the max over ranks counts; the region with the
@@ -122,7 +122,7 @@ def parse_args(argv=None):
                     help="rotating input sets (0 = enough for >= 512 MiB of distinct reads per rank)")
     ap.add_argument("--out-sets", type=int, default=0,
                     help="rotating output sets (0 = enough for >= 512 MiB of distinct writes per rank)")
-    ap.add_argument("--repeats", type=int, default=5,
+    ap.add_argument("--repeats", type=int, default=7,
                     help="timed regions of K steps each (the median region is the result, SURVEY 8d)")
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the memory-system twin (roofline.ceiling_measured)")

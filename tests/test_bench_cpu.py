@@ -39,9 +39,9 @@ def test_gpus_flag_spawns_ranks(n):
     # R timed regions of exactly K steps, the median one is the result
     # (per region the slowest rank counts; per_rank holds every rank in that region)
     rep = d["repeats"]
-    assert rep["regions"] == 5 and rep["steps_per_region"] == 2
+    assert rep["regions"] == 7 and rep["steps_per_region"] == 2
     by = rep["ms_per_step_by_region"]
-    assert len(by) == 5 and d["ms_per_step"] == pytest.approx(sorted(by)[2])
+    assert len(by) == 7 and d["ms_per_step"] == pytest.approx(sorted(by)[3])
     # value = all ranks' elements / the slowest rank's time
     slowest = max(r["ms_per_step"] for r in d["per_rank"])
     assert d["ms_per_step"] == pytest.approx(slowest)

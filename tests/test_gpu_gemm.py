@@ -955,3 +955,22 @@ def test_check_gemm_workspaces_raises_on_a_set_error_word(coracle, gpu):
     with pytest.raises(RuntimeError, match="split-K"):
         check_gemm_workspaces()
     assert check_gemm_workspaces() is None
+
+
+def test_release_gemm_workspaces_empties_the_cache(gpu):
+    """release_gemm_workspaces() synchronises the cached workspaces' streams and forgets
+    them (for callers that destroy their own external streams); nf4_linear then builds a
+    fresh one on its next call."""
+    from nf4_triton_dequantization_amd import kernel, nf4_linear, release_gemm_workspaces
+
+    M, N, K = 16, 4096, 4096
+    packed, a1, a2 = O.make_inputs(N, K, seed=78)
+    mod = make_module(packed, a1, a2, N, K, "bf16", gpu)
+    xt, _ = _x_bits(M, K, "bf16", seed=4)
+    y0 = nf4_linear(xt.to(gpu), mod)
+    assert kernel._GEMM_WS
+    release_gemm_workspaces()
+    assert not kernel._GEMM_WS
+    y1 = nf4_linear(xt.to(gpu), mod)
+    torch.cuda.synchronize()
+    assert kernel._GEMM_WS and torch.equal(y0.view(torch.int16), y1.view(torch.int16))
