@@ -142,6 +142,12 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_DECODE
 #define NF4_DQ_DECODE 1
 #endif
+//   NF4_DQ_SINGLE_FAST  1 (product): a wave with one tile skips the pipelined loop (next-tile
+//                       loads, dropped-store burst); 7.37 -> 7.23 us per streamed 4096^2
+//                       launch at K = 128 (profiles/r05/single_tile_fast_path.jsonl)
+#ifndef NF4_DQ_SINGLE_FAST
+#define NF4_DQ_SINGLE_FAST 1
+#endif
 //   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
@@ -403,10 +409,15 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
     __amdgpu_buffer_rsrc_t rpa, roa;
     make_rsrcs<DT>(bt, ca.k, rpa, roa);
     TileIn A = tile_load<DT, MODE>(bt.d[ca.k], rpa, ca.base, lane);
+    // Does this wave walk more than one tile?  (wave-uniform; at 4096^2 every wave has
+    // exactly one.)  A one-tile wave skips the pipelined loop: no loads of a next tile
+    // past the end and no dropped store burst below -- half of its vector-memory
+    // instructions otherwise.
+    const bool multi = !NF4_DQ_SINGLE_FAST || ca.t + nwaves < bt.total_tiles;
     // Out-of-range (dropped) stores with the loop body's count: loop entry then
     // looks like the back edge to hipcc's waitcnt pass ([loads][stores]), so the
     // in-loop waits count past the previous tile's stores instead of draining them.
-    {
+    if (multi) {
         const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int j = 0; j < kU; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, roa, 0xFFFFF000u + 16u * j, 0, kAuxStore);
@@ -429,6 +440,18 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
         NF4_FSTAMP(1, 0ull);
         NF4_FSTAMP(2, NF4_FNOW());
         NF4_FSTAMP(3, 0ull);
+        return;
+    }
+    if (!multi) {
+        if constexpr (kTbl) tile_finish_tbl<DT, MODE>(bt.d[ca.k], roa, A, ca.base, lane, code2s, tc);
+        else tile_finish<DT, MODE>(bt.d[ca.k], roa, lut, A, ca.base, lane, code2s);
+#if NF4_FLAT_STAMPS
+        NF4_FSTAMP(1, NF4_FNOW());
+        __builtin_amdgcn_s_waitcnt(0);
+        NF4_FSTAMP(0, t_entry);
+        NF4_FSTAMP(2, NF4_FNOW());
+        NF4_FSTAMP(3, 1ull);
+#endif
         return;
     }
     while (true) {

@@ -15,6 +15,7 @@
 // Round 5 also measured store delays, scale-gather buffer loads / policies, a table decode
 // without the code table and its barrier, and synchronised stores through hooks removed
 // after measurement (profiles/r05/; the hooks are in git history at 914c6b8).
+//   DQV_SINGLE=1   one-tile waves skip the pipelined loop
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
@@ -37,6 +38,9 @@
 
 #ifdef DQV_NOSCALE
 #define NF4_DQ_ABL_NOSCALE DQV_NOSCALE
+#endif
+#ifdef DQV_SINGLE
+#define NF4_DQ_SINGLE_FAST DQV_SINGLE
 #endif
 #ifdef DQV_DEC
 #define NF4_DQ_DECODE DQV_DEC
