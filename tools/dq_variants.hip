@@ -16,6 +16,7 @@
 // without the code table and its barrier, and synchronised stores through hooks removed
 // after measurement (profiles/r05/; the hooks are in git history at 914c6b8).
 //   DQV_SINGLE=1   one-tile waves skip the pipelined loop
+//   DQV_FASTIDX=1  reference-mode scale indices through the host-proven shortcuts
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
@@ -41,6 +42,12 @@
 #endif
 #ifdef DQV_SINGLE
 #define NF4_DQ_SINGLE_FAST DQV_SINGLE
+#endif
+#ifdef DQV_FASTIDX
+#define NF4_DQ_FAST_INDEX DQV_FASTIDX
+#endif
+#ifdef DQV_GDELAY
+#define NF4_DQ_GATHER_DELAY DQV_GDELAY
 #endif
 #ifdef DQV_DEC
 #define NF4_DQ_DECODE DQV_DEC
