@@ -59,15 +59,7 @@ struct Desc {
     uint32_t blk_shift;      // log2(bytes per scale block)
     uint32_t blk2_shift;     // bnb: log2(blocksize2)
     uint32_t blk_base;       // scale blocks before this piece (a matrix above kPieceBytes is several pieces)
-    uint32_t idx_fast;       // ref: kIdxA1Direct | kIdxA2Quarter | kIdxA2Mask (host-proven index shortcuts)
-    uint32_t n2_mask;        // ref, kIdxA2Mask: n2 - 1 (n2 a power of two)
 };
-
-// Reference-mode index shortcuts the host proves per matrix (ref_desc): the absmax index
-// (r*bpr + b) mod nb is the block index g itself when nb covers every block; the nested
-// index (r*G + b/4) mod n2 is (g/4) mod n2 when bpr % 4 == 0 (G = bpr/4), a mask when n2
-// is a power of two.  Same indices, fewer VALU (three magic-number divisions -> one shift).
-constexpr uint32_t kIdxA1Direct = 1u, kIdxA2Quarter = 2u, kIdxA2Mask = 4u;
 
 // Diagnostic build only (tools/Makefile `stamps`): per-wave s_memrealtime stamps of
 // the flat kernel -- entry, first tile decoded and stored (its loads arrived), exit
@@ -156,15 +148,6 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_SINGLE_FAST
 #define NF4_DQ_SINGLE_FAST 1
 #endif
-//   NF4_DQ_FAST_INDEX   1: reference-mode scale indices through the host-proven shortcuts
-//                       (Desc::idx_fast) instead of three magic-number divisions
-#ifndef NF4_DQ_FAST_INDEX
-#define NF4_DQ_FAST_INDEX 0
-#endif
-//   NF4_DQ_GATHER_DELAY > 0: s_sleep(n) between a tile's packed loads and its scale gathers
-#ifndef NF4_DQ_GATHER_DELAY
-#define NF4_DQ_GATHER_DELAY 0
-#endif
 //   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
@@ -235,23 +218,18 @@ __device__ __forceinline__ TileIn tile_load(const Desc& D, __amdgpu_buffer_rsrc_
         }
     };
     if constexpr (!NF4_DQ_SCALE_FIRST) packed_loads();
-    if constexpr (NF4_DQ_GATHER_DELAY > 0) __builtin_amdgcn_s_sleep(NF4_DQ_GATHER_DELAY);
     const uint32_t g = tile_block<DT>(D, base, lane);
     if constexpr (NF4_DQ_ABL_NOSCALE) {
         in.a1 = g & 255u;
         in.a2 = 0.01f;
     } else if constexpr (MODE == kRef) {
-        const uint8_t* pa1;
-        const float* pa2;
-        if (NF4_DQ_FAST_INDEX && (D.idx_fast & kIdxA2Quarter)) {  // wave-uniform
-            pa1 = D.a1 + ((D.idx_fast & kIdxA1Direct) ? g : fmodu(g, D.nb));
-            pa2 = D.a2 + ((D.idx_fast & kIdxA2Mask) ? ((g >> 2) & D.n2_mask) : fmodu(g >> 2, D.n2));
-        } else {
-            const uint32_t r = fdiv(g, D.bpr);
-            const uint32_t b = g - r * D.bpr.d;
-            pa1 = D.a1 + fmodu(g, D.nb);
-            pa2 = D.a2 + fmodu(r * D.groups + (b >> 2), D.n2);
-        }
+        // (host-proven shortcuts for these indices -- one shift instead of the three
+        // magic-number divisions -- measured no faster: the gathers issued earlier cost as
+        // much as they save, profiles/r05/fast_index_ab.jsonl, gather_delay_variants.jsonl)
+        const uint32_t r = fdiv(g, D.bpr);
+        const uint32_t b = g - r * D.bpr.d;
+        const uint8_t* pa1 = D.a1 + fmodu(g, D.nb);
+        const float* pa2 = D.a2 + fmodu(r * D.groups + (b >> 2), D.n2);
         if constexpr (NF4_DQ_SCALE_NT) {
             in.a1 = __builtin_nontemporal_load(pa1);
             in.a2 = __builtin_nontemporal_load(pa2);
@@ -731,7 +709,7 @@ int launch_flat_matrix(const Desc& proto, int64_t m, int64_t n, int32_t dtype, i
 }
 
 Desc ref_desc(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int64_t nb, const float* a2,
-              int64_t n2, void* out, int64_t m, int64_t n) {
+              int64_t n2, void* out, int64_t n) {
     Desc d{};
     d.packed = reinterpret_cast<const uint32_t*>(packed);
     d.a1 = a1;
@@ -745,15 +723,6 @@ Desc ref_desc(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int6
     d.n2 = make_fastdiv((uint32_t)(n2 > (int64_t(1) << 31) ? (int64_t(1) << 31) : n2));
     d.bpr = make_fastdiv((uint32_t)bpr);
     d.blk_shift = 5;  // 64 elements = 32 packed bytes
-    if (bpr % 4 == 0) {
-        d.idx_fast = kIdxA2Quarter;
-        if (nb >= m * bpr) d.idx_fast |= kIdxA1Direct;  // every block index < nb: no wrap
-        if ((n2 & (n2 - 1)) == 0) {
-            d.idx_fast |= kIdxA2Mask;
-            // indices g/4 stay below 2^29: a power-of-two n2 beyond 2^31 never wraps them
-            d.n2_mask = n2 > (int64_t(1) << 31) ? 0x7FFFFFFFu : (uint32_t)(n2 - 1);
-        }
-    }
     return d;
 }
 
@@ -763,7 +732,7 @@ int ref_impl(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int64
     if (rc || m == 0 || n == 0) return rc;
     if (!a1 || !a2 || nb <= 0 || n2 <= 0) return NF4DQ_ERR_ARG;
     if (flat_eligible(packed, packed_len, out, m, n))
-        return launch_flat_matrix(ref_desc(packed, packed_len, a1, nb, a2, n2, out, m, n), m, n, dtype, kRef, cfg, st);
+        return launch_flat_matrix(ref_desc(packed, packed_len, a1, nb, a2, n2, out, n), m, n, dtype, kRef, cfg, st);
     RowsArgs A{};
     A.packed = packed;
     A.a1 = a1;
@@ -815,7 +784,7 @@ int nf4_dequant_single(const uint8_t* packed, int64_t packed_len, const float* a
     if (absmax_len % m || absmax_len / m < bpr) return NF4DQ_ERR_SHAPE;
     const int64_t rs = absmax_len / m;
     if (flat_eligible(packed, packed_len, out, m, n) && absmax_len < (int64_t(1) << 31)) {
-        Desc d = ref_desc(packed, packed_len, nullptr, 1, absmax, 1, out, m, n);
+        Desc d = ref_desc(packed, packed_len, nullptr, 1, absmax, 1, out, n);
         d.n2 = make_fastdiv((uint32_t)rs);
         return launch_flat_matrix(d, m, n, out_dtype, kSingle, kDefaultCfg, st);
     }
@@ -861,7 +830,7 @@ int nf4_dequant_ref_batched(const nf4_matrix_desc* descs, int32_t count, int32_t
             continue;
         }
         const int rc = append_pieces(b, ref_desc(d.packed, d.packed_len, d.absmax_q, d.nb, d.absmax2, d.n2, d.out,
-                                                 d.m, d.n), d.m, d.n, out_dtype, kRef, st);
+                                                 d.n), d.m, d.n, out_dtype, kRef, st);
         if (rc) return rc;
     }
     if (b.count) return launch_flat_batch(b, out_dtype, kRef, kDefaultCfg, st);
