@@ -99,7 +99,7 @@ for stage in "$@"; do
         trace bench_8192 nf4_flat_kernel 64 300 -- bench.py --m 8192 --n 8192 --steps 64 --no-cpu-baseline ;;
     rocprof)
         trace bench nf4_flat_kernel 200 300 -- bench.py --steps 200 --repeats 1 --no-cpu-baseline --no-c5 \
-            --no-ceiling --spin-us-per-launch 150
+            --no-ceiling --spin-us-per-launch 500
         python3 tools/rocprof_summary.py "$O/prof_bench" nf4_flat_kernel "$O/rocprof_bench_summary.json" \
             "$O/rocprof_bench_kernel_stats.csv" --last 200 > /dev/null ;;
     pmc)  # headline HBM traffic (FETCH_SIZE / WRITE_SIZE passes, calibrated) + decode-GEMM SQ counters
