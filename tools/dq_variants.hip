@@ -43,6 +43,12 @@
 #ifdef DQV_SINGLE
 #define NF4_DQ_SINGLE_FAST DQV_SINGLE
 #endif
+#ifdef DQV_BNBCODE
+#define NF4_DQ_BNB_CODE DQV_BNBCODE
+#endif
+#ifdef DQV_GDELAY
+#define NF4_DQ_GATHER_DELAY DQV_GDELAY
+#endif
 #ifdef DQV_DEC
 #define NF4_DQ_DECODE DQV_DEC
 #endif

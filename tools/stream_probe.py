@@ -13,6 +13,8 @@ Kernels (tools/stream_probe.hip, ``tools/_build/libstreamprobe.so``):
   ``mixs:ST:CH``     mix with the product's scale gathers and CH dependent VALU ops per
                      stored dword (stand-in for decode latency)
   ``prod``           nf4_dequant_ref (the product, bf16); ``prod16`` the same with fp16 output
+  ``bnb``            nf4_dequant_bnb (bitsandbytes semantics, blocksize 64 / nested 256),
+                     bf16; ``<lib>@bnb`` the same through a --libs library
   ``<lib>``          nf4_dequant_ref of a library given with --libs (basename without
                      ``libnf4dq_`` / ``.so``); ``<lib>@16`` the same with fp16 output
 
@@ -43,6 +45,7 @@ import workloads as W  # noqa: E402
 from nf4_triton_dequantization_amd import _lib  # noqa: E402
 
 PEAK = 8e12
+BNB_OFFSET = 0.0123
 KIND = {"mix": 0, "rd": 1, "wr": 2, "empty": 3, "emptydiv": 4, "empty1": 5, "mixs": 6}
 
 
@@ -87,12 +90,26 @@ def main():
     ins = [(q0, a1_0, a2_0)] + [(q0.clone(), a1_0.clone(), a2_0.clone()) for _ in range(PI - 1)]
     outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(PO)]
     sink = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+    # bitsandbytes semantics (spec "bnb" / "<lib>@bnb"): the nested code and its absmax
+    code2_t = torch.linspace(-1, 1, 256, device=dev, dtype=torch.float32)
+    bnb_a2 = torch.rand((nb + 255) // 256, device=dev) * 0.01 + 1e-3
     # mixs: absmax bytes then 1024 nested absmax floats in one buffer
     scal = torch.cat([a1_0.view(torch.uint8), a2_0[:1024].view(torch.uint8)]) if nb % 4 == 0 else None
     torch.cuda.synchronize()
 
     def maker(spec):
         parts = spec.split(":")
+        if parts[0] == "bnb" or parts[0].endswith("@bnb"):
+            L = libs["prod" if parts[0] == "bnb" else parts[0][:-4]]
+
+            def f(i):
+                q, a1, _ = ins[i % PI]
+                rc = L.nf4_dequant_bnb(q.data_ptr(), a1.data_ptr(), nb, code2_t.data_ptr(), bnb_a2.data_ptr(),
+                                       bnb_a2.numel(), ctypes.c_float(BNB_OFFSET), outs[i % PO].data_ptr(),
+                                       _lib.BF16, m * n, 64, 256, sp)
+                if rc:
+                    raise RuntimeError(_lib.strerror(rc))
+            return f
         name16 = parts[0][:-3] if parts[0].endswith("@16") else None
         if parts[0] in ("prod", "prod16") or parts[0] in libs or name16 in libs:
             L = libs["prod" if parts[0] == "prod16" else (name16 or parts[0])]
@@ -168,6 +185,16 @@ def main():
 
     checked = {}
     for s in specs:
+        if s == "bnb" or s.endswith("@bnb"):
+            outs[0].zero_()
+            fns[s](0)
+            torch.cuda.synchronize()
+            r = 32
+            want = Ora.COracle().dequant_bnb(p0[: r * n // 2], a10, code2_t.cpu().numpy(), bnb_a2.cpu().numpy(),
+                                             np.float32(BNB_OFFSET), r * n, Ora.BF16, 64, 256)
+            got = outs[0][:r].contiguous().view(torch.int16).cpu().numpy().view(np.uint16).reshape(-1)
+            checked[s] = bool(np.array_equal(got, want.reshape(-1)))
+            continue
         if s.split(":")[0] in ("prod", "prod16") or s in libs or s[:-3] in libs:
             outs[0].zero_()
             fns[s](0)
