@@ -148,18 +148,6 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_SINGLE_FAST
 #define NF4_DQ_SINGLE_FAST 1
 #endif
-//   NF4_DQ_BNB_CODE     bitsandbytes mode's 256-entry nested code into LDS: 0 = every thread
-//                       loads one float after the first tile's loads; 1 = wave 0 loads the
-//                       1 KiB with one 16-B load per lane ahead of everything; 2 = ablation
-//                       (no code table: wrong results, timing only)
-#ifndef NF4_DQ_BNB_CODE
-#define NF4_DQ_BNB_CODE 0
-#endif
-//   NF4_DQ_GATHER_DELAY bitsandbytes mode: s_sleep(n) between a tile's packed loads and its
-//                       absmax gathers
-#ifndef NF4_DQ_GATHER_DELAY
-#define NF4_DQ_GATHER_DELAY 0
-#endif
 //   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
@@ -230,7 +218,6 @@ __device__ __forceinline__ TileIn tile_load(const Desc& D, __amdgpu_buffer_rsrc_
         }
     };
     if constexpr (!NF4_DQ_SCALE_FIRST) packed_loads();
-    if constexpr (NF4_DQ_GATHER_DELAY > 0 && MODE == kBnb) __builtin_amdgcn_s_sleep(NF4_DQ_GATHER_DELAY);
     const uint32_t g = tile_block<DT>(D, base, lane);
     if constexpr (NF4_DQ_ABL_NOSCALE) {
         in.a1 = g & 255u;
@@ -336,11 +323,7 @@ __device__ __forceinline__ void tile_finish_tbl(const Desc& D, __amdgpu_buffer_r
     if constexpr (MODE == kRef) {
         s = ((float)in.a1 / 127.0f) * in.a2;  // IEEE division (:45, :270), then fp32 multiply
     } else if constexpr (MODE == kBnb) {
-        if constexpr (NF4_DQ_BNB_CODE == 2) {
-            s = (float)in.a1 * in.a2 + D.offset;
-        } else {
-            s = code2s[in.a1] * in.a2 + D.offset;
-        }
+        s = code2s[in.a1] * in.a2 + D.offset;
     } else {
         s = in.a2;
     }
@@ -421,10 +404,6 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
 #endif
     const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kFlatWaves + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * kFlatWaves;
-    u32x4 code2v = {0u, 0u, 0u, 0u};
-    if constexpr (MODE == kBnb && NF4_DQ_BNB_CODE == 1) {
-        if (threadIdx.x < 64u) code2v = reinterpret_cast<const u32x4*>(bt.d[0].code2)[threadIdx.x];
-    }
 
     // First tile's loads go out before anything else (a wave without work
     // issues them past the buffer range: no traffic); the LUT write and the
@@ -449,10 +428,10 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
     // (the table decode could take its two codes from immediates and skip this table and
     // the barrier: measured 8 % slower, profiles/r05/nolut_scalefirst_variants.jsonl)
     write_lut(lut);
-    if constexpr (MODE == kBnb && NF4_DQ_BNB_CODE == 0) {  // every piece of a bitsandbytes stream carries the same code
+    if constexpr (MODE == kBnb) {  // every piece of a bitsandbytes stream carries the same code
+        // (one 16-B load per lane of wave 0 ahead of everything measured slower, and no
+        // table at all only 0.6 % faster: profiles/r05/bnb_mode_code_table.jsonl)
         for (uint32_t i = threadIdx.x; i < 256u; i += kFlatWg) code2s[i] = bt.d[0].code2[i];
-    } else if constexpr (MODE == kBnb && NF4_DQ_BNB_CODE == 1) {
-        if (threadIdx.x < 64u) reinterpret_cast<u32x4*>(code2s)[threadIdx.x] = code2v;
     }
     __syncthreads();
     TblCtx tc{};

@@ -15,7 +15,8 @@
 // Round 5 also measured store delays, scale-gather buffer loads / policies, a table decode
 // without the code table and its barrier, and synchronised stores through hooks removed
 // after measurement (profiles/r05/; the hooks are in git history at 914c6b8), and scale-index shortcuts and
-// gather delays (at 414c083).
+// gather delays (at 414c083), bitsandbytes-mode code-table loads and gather
+// delays (at 99ed841).
 //   DQV_SINGLE=1   one-tile waves skip the pipelined loop
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
@@ -42,12 +43,6 @@
 #endif
 #ifdef DQV_SINGLE
 #define NF4_DQ_SINGLE_FAST DQV_SINGLE
-#endif
-#ifdef DQV_BNBCODE
-#define NF4_DQ_BNB_CODE DQV_BNBCODE
-#endif
-#ifdef DQV_GDELAY
-#define NF4_DQ_GATHER_DELAY DQV_GDELAY
 #endif
 #ifdef DQV_DEC
 #define NF4_DQ_DECODE DQV_DEC
