@@ -21,11 +21,14 @@
 //  * one lane per 64-element block computes the block's scale (absmax byte,
 //    nested absmax, IEEE fp32 division by 127 -- never a reciprocal), and the
 //    eight lanes that own the block's dwords fetch it with ds_bpermute.
-//  * the 16-entry NF4 table sits in LDS: 16 consecutive fp32 = 16 distinct
-//    banks, repeated indices broadcast, so the lookups are conflict-free.
-//  * fp32 -> bf16/fp16 through v_cvt_pk_{bf16,f16}_f32 (round to nearest even),
-//    two outputs per instruction, high nibble -> even column (fp32 output, as
-//    quant_state.dtype = torch.float32 asks, is stored unrounded).
+//  * 16-bit outputs decode through a per-block table (round 5): the 8 lanes of a
+//    64-element block round its 16 possible outputs (fp32 product, then
+//    v_cvt_pk_{bf16,f16}_f32, round to nearest even) into 32 bytes of LDS, and every
+//    output is one 16-bit lookup whose address is a single v_perm_b32; high nibble
+//    -> even column.  fp32 output (quant_state.dtype = torch.float32) looks the code
+//    up in the 16-entry LDS table and stores the product unrounded.
+//  * a wave that owns one tile (every wave at 4096^2) runs it straight through; waves
+//    with several walk the software-pipelined loop.
 //  * batched: up to NF4DQ_BATCH_MAX matrices per launch in the kernel
 //    arguments; a wave finds its matrix by scanning scalar tile offsets.
 //  * "rows" kernels: any other shape (partial blocks, padded rows, odd n) --
@@ -106,14 +109,25 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 }
 
 // Variant hooks of the flat kernel: the product values by default.  tools/dq_variants.hip
-// redefines them to build A/B libraries (tools/_build/libnf4dq_dqv_<x>.so, timing in the
-// HBM-streamed regime with tools/cache_ab.py --libs); nothing in the product sets them.
+// redefines them to build A/B libraries (tools/_build/libnf4dq_dqv_<x>.so, timed in the
+// HBM-streamed regime by tools/stream_probe.py / cache_ab.py --libs); nothing in the
+// product sets them.  Hooks whose variants measured slower were removed after measurement
+// (profiles/r05/README.md names them and the commits that still have them).
 //   NF4_DQ_FLAT_WAVES   waves per workgroup of the flat kernel (4)
 //   NF4_DQ_U            packed dwords per lane per tile (4: 1 KiB of packed bytes per wave)
 //   NF4_DQ_AUX_STORE    cache-policy bits of the output stores (18 = sc1 + nt)
 //   NF4_DQ_AUX_LOAD     cache-policy bits of the packed-weight loads (2 = nt)
 //   NF4_DQ_SCALE_FIRST  1: a tile's absmax / nested-scale loads go out before its packed loads
 //   NF4_DQ_SCALE_NT     1: the absmax / nested-scale gathers carry the nt policy too
+//   NF4_DQ_DECODE       16-bit outputs: 1 (product) = per-block table of the 16 rounded
+//                       outputs in LDS (tile_finish_tbl); 0 = code lookup per nibble + fp32
+//                       multiply + rounding per output (rounds 1-4; fp32 output always takes
+//                       this path).  HBM-streamed 4096^2 bf16: 7.33-7.36 us per launch vs
+//                       7.62-7.65 (profiles/r05/dequant_decode_ab.jsonl)
+//   NF4_DQ_SINGLE_FAST  1 (product): a wave with one tile skips the pipelined loop (next-tile
+//                       loads, dropped-store burst); 7.33 -> 7.22 us per streamed 4096^2
+//                       launch at K = 128 (profiles/r05/single_tile_fast_path_ab.jsonl)
+//   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
 #ifndef NF4_DQ_FLAT_WAVES
 #define NF4_DQ_FLAT_WAVES 4
 #endif
@@ -132,23 +146,12 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_SCALE_NT
 #define NF4_DQ_SCALE_NT 0
 #endif
-//   NF4_DQ_DECODE       16-bit outputs: 1 (product) = per-block table of the 16 rounded
-//                       outputs in LDS, built by the block's 8 lanes (2 products + 1 rounding
-//                       each), then one 16-bit lookup per nibble whose LDS address is one
-//                       v_perm_b32; 0 = code lookup per nibble + fp32 multiply + rounding per
-//                       output (rounds 1-4; fp32 output always takes this path).  Round 5,
-//                       HBM-streamed 4096^2 bf16: 7.33-7.36 us per launch vs 7.62-7.65
-//                       (profiles/r05/dequant_decode_ab.jsonl)
 #ifndef NF4_DQ_DECODE
 #define NF4_DQ_DECODE 1
 #endif
-//   NF4_DQ_SINGLE_FAST  1 (product): a wave with one tile skips the pipelined loop (next-tile
-//                       loads, dropped-store burst); 7.37 -> 7.23 us per streamed 4096^2
-//                       launch at K = 128 (profiles/r05/single_tile_fast_path.jsonl)
 #ifndef NF4_DQ_SINGLE_FAST
 #define NF4_DQ_SINGLE_FAST 1
 #endif
-//   NF4_DQ_ABL_NOSCALE  ablation (wrong results, tools only): no absmax / nested-absmax loads
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
 #endif
@@ -160,8 +163,10 @@ constexpr int kU = NF4_DQ_U;  // packed dwords (fp32 output: words) per lane per
 
 // Cache-policy bits of the buffer instructions (aux operand, gfx950 CPol):
 // 2 = nt (streaming), 16 = sc1.  Output stores are sc1+nt: a write-once stream,
-// not kept in the XCD L2 (+25-30 % over default-policy stores, and 1-2 % over nt
-// alone; profiles/r01/tune_sweep.log).
+// not kept in the XCD L2 (+25-30 % over default-policy stores, profiles/r01/tune_sweep.log).
+// Round 5, weights streamed from HBM: nt-only stores make the memory-system twin 2 %
+// faster but the product 4-5 % slower at 4096^2 and 8192^2 alike (they interact with the
+// scale gathers; profiles/r05/decode_store_variants_4096.jsonl, store_policy_large.jsonl).
 constexpr int kAuxStore = NF4_DQ_AUX_STORE;
 // Packed-weight loads are nt (streaming; round 4): a streamed model reads each weight
 // once, from HBM.  With the default policy a 4096^2 launch whose weights come from
