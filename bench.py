@@ -623,7 +623,10 @@ def twin_ceiling(args, mat, dev, world, rank, alg, kernel_us):
     return {"kernel": "twin_mix (tools/stream_probe.hip): the flat kernel's loads and stores, no decode",
             "launch_us": us, "achieved": alg / (us * 1e-6) / 1e9, "frac": alg / (us * 1e-6) / PEAK_HBM,
             "kernel_over_twin": kernel_us / us,
-            "method": "same rotation, K, repeats, lead and spin as the headline, timed right after it"}
+            "method": "same rotation, K, repeats, lead and spin as the headline, timed right after it",
+            "note": ("the twin has the product's loads and stores but no scale gathers and no decode; "
+                     "since round 5's one-tile path the product is faster than it (kernel_over_twin < 1), "
+                     "so it bounds the access pattern, not the kernel (DESIGN.md section 4)")}
 
 
 def distribute_stats(all_mats, rank, world, dev, dt, cpu):
