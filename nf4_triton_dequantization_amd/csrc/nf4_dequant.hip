@@ -16,7 +16,7 @@
 //    every HBM line is written whole by one store instruction.  Loads and
 //    stores are buffer instructions (range-checked: partial tiles need no
 //    predicates), output stores are non-temporal (written once, streamed),
-//    and the persistent wave loop is software-pipelined: the next tile's loads
+//    and a capped grid's wave loop is software-pipelined: the next tile's loads
 //    are in flight while the current tile is decoded and stored.
 //  * one lane per 64-element block computes the block's scale (absmax byte,
 //    nested absmax, IEEE fp32 division by 127 -- never a reciprocal), and the
@@ -27,8 +27,9 @@
 //    output is one 16-bit lookup whose address is a single v_perm_b32; high nibble
 //    -> even column.  fp32 output (quant_state.dtype = torch.float32) looks the code
 //    up in the 16-entry LDS table and stores the product unrounded.
-//  * a wave that owns one tile (every wave at 4096^2) runs it straight through; waves
-//    with several walk the software-pipelined loop.
+//  * the default grid gives every wave exactly one tile (tiles/4 workgroups), which it
+//    runs straight through; only a grid capped through nf4_dequant_ref_cfg makes waves
+//    walk several tiles in the software-pipelined loop.
 //  * batched: up to NF4DQ_BATCH_MAX matrices per launch in the kernel
 //    arguments; a wave finds its matrix by scanning scalar tile offsets.
 //  * "rows" kernels: any other shape (partial blocks, padded rows, odd n) --
@@ -391,11 +392,11 @@ __device__ __forceinline__ void make_rsrcs(const Batch<MAXB>& bt, uint32_t k, __
     ro = __builtin_amdgcn_make_buffer_rsrc((void*)bt.d[k].out, 0, bt.d[k].nbytes * kOB, kRsrcFlags);
 }
 
-// Persistent, software-pipelined flat kernel.  Each wave walks tiles
-// t, t + nwaves, ... (one tile per wave unless the grid is capped); the loop is
-// unrolled by two with the tiles in two register sets (A, B) so that tile i+1's
-// loads are in flight while tile i is decoded and stored, with no register copies
-// (a copy would force a wait on the loads it copies).
+// The flat kernel.  Wave t owns tile t; with the default grid that is its only tile and
+// it runs it straight through.  Under a capped grid (nf4_dequant_ref_cfg) waves walk
+// tiles t, t + nwaves, ... in a loop unrolled by two with the tiles in two register
+// sets (A, B), so that tile i+1's loads are in flight while tile i is decoded and
+// stored, with no register copies (a copy would force a wait on the loads it copies).
 template <int DT, int MODE, int MAXB>
 __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt) {
     __shared__ __attribute__((aligned(16))) float lut[16];
@@ -417,10 +418,10 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
     __amdgpu_buffer_rsrc_t rpa, roa;
     make_rsrcs<DT>(bt, ca.k, rpa, roa);
     TileIn A = tile_load<DT, MODE>(bt.d[ca.k], rpa, ca.base, lane);
-    // Does this wave walk more than one tile?  (wave-uniform; at 4096^2 every wave has
-    // exactly one.)  A one-tile wave skips the pipelined loop: no loads of a next tile
-    // past the end and no dropped store burst below -- half of its vector-memory
-    // instructions otherwise.
+    // Does this wave walk more than one tile?  (wave-uniform; with the default, uncapped
+    // grid every wave has exactly one.)  A one-tile wave skips the pipelined loop: no
+    // loads of a next tile past the end and no dropped store burst below -- half of its
+    // vector-memory instructions otherwise.
     const bool multi = !NF4_DQ_SINGLE_FAST || ca.t + nwaves < bt.total_tiles;
     // Out-of-range (dropped) stores with the loop body's count: loop entry then
     // looks like the back edge to hipcc's waitcnt pass ([loads][stores]), so the
