@@ -314,6 +314,7 @@ __device__ __forceinline__ void tile_finish(const Desc& D, __amdgpu_buffer_rsrc_
 // barrier; the next dword's table reuses the region after this one's reads.
 typedef uint16_t __attribute__((may_alias)) u16_alias;  // table entries are written as dwords
 typedef uint32_t __attribute__((may_alias)) u32_alias;
+typedef uint32_t u32x4_alias __attribute__((ext_vector_type(4), may_alias));
 
 struct TblCtx {
     char* tbl;    // LDS base of the workgroup's tables
@@ -500,7 +501,9 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
 #endif
 }
 
-// Any shape, reference / single-quant semantics: one thread per packed byte.
+// Any shape, reference / single-quant semantics: one thread per packed byte.  Only for
+// matrices past the chunk kernel's 32-bit index limits (below) or when a tuning call
+// asks for it (NF4DQ_CFG_ROWS).
 struct RowsArgs {
     const uint8_t* packed;
     const uint8_t* a1;
@@ -531,6 +534,352 @@ __global__ __launch_bounds__(kWg) void nf4_rows_kernel(const RowsArgs A) {
         const int64_t c = 2 * j;
         store1<DT>(A.out, r * A.n + c, lut[byte >> 4] * s);
         if (c + 1 < A.n) store1<DT>(A.out, r * A.n + c + 1, lut[byte & 15u] * s);
+    }
+}
+
+// The chunk kernel (round 5): every shape the flat kernel does not take -- n % 64 != 0
+// (rows end in a partial 64-column block), padded rows, unaligned pointers -- with
+// reference / single-quant semantics.  Each row's packed bytes are cut into 4-byte
+// chunks (L = ceil(ceil(n/2) / 4) per row); chunk c = r * L + q holds columns 8q .. 8q+7
+// of row r, all inside 64-column block q / 8.  A wave owns 256 consecutive chunks, lane l
+// chunk 64 j + l at step j -- the flat kernel's tile with rows cut out of the stream: each
+// load instruction walks a row's bytes contiguously, and when n % 8 == 0 the output of
+// the wave is the dense range 8c .. 8c+7 of 16-byte stores, as in the flat kernel.  Blocks
+// no longer line up with groups of 8 lanes: each lane fetches its block's scale from the
+// lane that gathered it (below) and decodes per nibble.  Partial chunks (n % 8 != 0) store 4- or 2-byte pieces, each past-n
+// piece sent out of the buffer range (dropped) instead of branched around.  The buffer
+// bases are the wave's first row / output element (scalar 64-bit), so only the offsets
+// within one wave's span are 32-bit.
+struct ChunkArgs {
+    const uint8_t* packed;
+    const uint8_t* a1;
+    const float* a2;
+    void* out;
+    uint64_t packed_len;  // bytes (the load range)
+    uint64_t out_elems;   // m * n
+    uint32_t stride;      // packed bytes per row
+    uint32_t n;           // columns
+    uint32_t chunks;      // m * L
+    FastDiv L;            // chunks per row
+    FastDiv bpr;          // 64-column blocks per row
+    uint32_t groups;      // ceil(bpr / 4)
+    FastDiv nb, n2;       // ref: moduli of the absmax / nested-absmax indices
+    uint32_t rs;          // single: absmax per row
+};
+
+constexpr uint32_t kDrop = 0xFFFFFFF0u;  // an offset past every range: load 0 / store dropped
+// Stores of pieces narrower than 16 bytes (one wave instruction writes every 4th / 8th piece
+// of its 1 KiB span) use the default policy, so that the L2 merges a line's pieces before
+// it goes to HBM: streamed (nt) partial-line writes made odd-n matrices 16x slower.
+constexpr int kAuxPiece = 0;
+#ifndef NF4_DQ_CHUNK_SYNC
+#define NF4_DQ_CHUNK_SYNC 0
+#endif
+#ifndef NF4_DQ_CHUNK_GATHER
+#define NF4_DQ_CHUNK_GATHER 0
+#endif
+
+inline __device__ uint32_t range32(uint64_t v) { return v > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)v; }
+
+// Block-table decode of one wave's 4 steps (16-bit output): lane i has rounded the 16
+// outputs of block g0 + i (fp32 products and RNE, as everywhere) into 32 bytes at the
+// wave's LDS region + 32 i.  Output (t = block - g0, code) is the 16-bit entry at region +
+// 256 (t >> 3) + 32 (t & 7) + 2 code: the low byte is the code byte (2 code, from (w >> 3)
+// or (w << 1) & 0x1E) ORed with 32 (t & 7) in every byte lane, and v_perm_b32 drops it
+// below region + 256 (t >> 3) -- one instruction per address, as in the flat kernel, and
+// no ds_bpermute of the scale.
+template <int DT>
+__device__ __forceinline__ void chunk_table_build(char* ctbl, uint32_t region, uint32_t lane, float sb) {
+    uint32_t e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        e[k] = pack2<DT>(__uint_as_float(kNf4Bits[2 * k]) * sb, __uint_as_float(kNf4Bits[2 * k + 1]) * sb);
+    u32x4_alias* dst = reinterpret_cast<u32x4_alias*>(ctbl + region + 32u * lane);
+    dst[0] = u32x4{e[0], e[1], e[2], e[3]};
+    dst[1] = u32x4{e[4], e[5], e[6], e[7]};
+}
+
+__device__ __forceinline__ void chunk_table_decode(const char* ctbl, uint32_t region, uint32_t w, uint32_t t,
+                                                   uint32_t (&p)[4]) {
+    t &= 63u;  // (lanes past the end: any table; their stores drop)
+    const uint32_t base = region + ((t >> 3) << 8);
+    const uint32_t rep = __builtin_amdgcn_perm(0u, (t & 7u) << 5, 0x00000000u);  // the byte in every lane
+    const uint32_t hb = ((w >> 3) & 0x1E1E1E1Eu) | rep;
+    const uint32_t lb = ((w << 1) & 0x1E1E1E1Eu) | rep;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t ah = __builtin_amdgcn_perm(hb, base, 0x03020104u + b);
+        const uint32_t al = __builtin_amdgcn_perm(lb, base, 0x03020104u + b);
+        const uint32_t vh = *reinterpret_cast<const u16_alias*>(ctbl + ah);
+        const uint32_t vl = *reinterpret_cast<const u16_alias*>(ctbl + al);
+        p[b] = vh | (vl << 16);
+    }
+}
+
+// The chunk kernel's dense form: 16-bit output, n % 8 == 0, packed rows of exactly 4 L
+// bytes, rows of >= 64 chunks, < 2 GiB each way.  Chunk c is then packed bytes 4c .. 4c+3
+// and output elements 8c .. 8c+7 -- the flat kernel's stream -- so the loads go out first
+// with no row arithmetic, the stores need none either, and only the scale blocks
+// (r * bpr + q / 8) follow the rows.
+template <int DT, int MODE>
+__global__ __launch_bounds__(kWg) void nf4_chunk_dense_kernel(const ChunkArgs A) {
+    __shared__ __attribute__((aligned(256))) char ctbl[4 * 2048];  // 64 block tables per wave
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t cw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
+    const __amdgpu_buffer_rsrc_t rp =
+        __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, (uint32_t)A.packed_len, kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(A.out, 0, (uint32_t)(A.out_elems * 2u), kRsrcFlags);
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // (past the end: out of range, no traffic)
+        w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, 4u * (cw + 64u * j + lane), 0, kAuxLoad);
+    __builtin_amdgcn_sched_barrier(0);  // (the scheduler would hoist the scale gathers above them)
+    // The blocks of the wave's 256 chunks are consecutive and at most 38 (rows >= 64 chunks):
+    // lane i gathers block g0 + i's scale (cf. the general form below).
+    const uint32_t r0 = fdiv(cw, A.L);
+    const uint32_t q0 = cw - r0 * A.L.d;
+    const uint32_t cl = min(cw + 255u, A.chunks - 1u);
+    const uint32_t rl = fdiv(cl, A.L);
+    const uint32_t g0 = r0 * A.bpr.d + (q0 >> 3);
+    const uint32_t gl = rl * A.bpr.d + ((cl - rl * A.L.d) >> 3);
+    float sb;
+    {
+        const uint32_t g = min(g0 + lane, gl);
+        const uint32_t r = fdiv(g, A.bpr);
+        const uint32_t b = g - r * A.bpr.d;
+        if constexpr (MODE == kRef) {
+            const float q8 = (float)A.a1[fmodu(g, A.nb)];
+            sb = (q8 / 127.0f) * A.a2[fmodu(r * A.groups + (b >> 2), A.n2)];  // IEEE division (:45, :270)
+        } else {
+            sb = A.a2[r * A.rs + b];
+        }
+    }
+    uint32_t gsel[4];
+    {
+        uint32_t q = q0 + lane;
+        const bool wrap = q >= A.L.d;
+        q = wrap ? q - A.L.d : q;
+        uint32_t gr = (wrap ? A.bpr.d : 0u) + r0 * A.bpr.d - g0;  // r * bpr - g0
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j) {
+                q += 64u;
+                const bool wj = q >= A.L.d;
+                q = wj ? q - A.L.d : q;
+                gr += wj ? A.bpr.d : 0u;
+            }
+            gsel[j] = gr + (q >> 3);
+        }
+    }
+    const uint32_t region = (threadIdx.x >> 6) << 11;
+    chunk_table_build<DT>(ctbl, region, lane, sb);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t p[4];
+        chunk_table_decode(ctbl, region, w[j], gsel[j], p);
+        const u32x4 o = {p[0], p[1], p[2], p[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(o, ro, 16u * (cw + 64u * j + lane), 0, kAuxStore);
+    }
+}
+
+// LW: 4 = dword loads (packed and stride 4-byte aligned), 1 = byte loads.
+// SW: 16 = whole-chunk 16-byte stores (16-bit output: n % 8 == 0; fp32: n % 4 == 0, two
+// per chunk; output 16-byte aligned), 4 = 4-byte pieces (16-bit: pairs, n even), 2 = single
+// 16-bit elements (odd n).
+template <int DT, int MODE, int LW, int SW>
+__global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
+    __shared__ __attribute__((aligned(16))) float lut[16];
+    __shared__ __attribute__((aligned(256))) char ctbl[DT == NF4DQ_F32 ? 4 : 4 * 2048];  // 64 block tables per wave
+    constexpr uint32_t kOB = DT == NF4DQ_F32 ? 4u : 2u;  // output bytes per element
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t cw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
+    const uint32_t r0 = fdiv(cw, A.L);
+    const uint32_t q0 = cw - r0 * A.L.d;
+    const uint64_t pb = (uint64_t)r0 * A.stride;
+    const uint64_t e0 = (uint64_t)r0 * A.n + 8ull * q0;  // the wave's first output element
+    const __amdgpu_buffer_rsrc_t rp =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(A.packed + pb), 0, range32(A.packed_len - pb), kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((char*)A.out + e0 * kOB), 0, range32((A.out_elems - e0) * kOB), kRsrcFlags);
+    auto load_chunk = [&](uint32_t po) -> uint32_t {
+        if constexpr (LW == 4) {
+            return __builtin_amdgcn_raw_buffer_load_b32(rp, po, 0, kAuxLoad);
+        } else {
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rp, po + k, 0, 0) << (8 * k);  // (4 per line: cached)
+            return v;
+        }
+    };
+    // The blocks of the wave's chunks are consecutive (block g = r * bpr + q / 8 steps by one
+    // per 8 chunks, and from a row's last block to the next row's first): when they number
+    // at most 64, lane i gathers block g0 + i's scale once and the lanes fetch theirs with
+    // ds_bpermute, as in the flat kernel; a wider span (rows of a few chunks) gathers per lane.
+    const uint32_t cl = min(cw + 255u, A.chunks - 1u);
+    const uint32_t rl = fdiv(cl, A.L);
+    const uint32_t g0 = r0 * A.bpr.d + (q0 >> 3);
+    const uint32_t gl = rl * A.bpr.d + ((cl - rl * A.L.d) >> 3);
+    const bool shared = gl - g0 < 64u;
+    // The shared gathers' indices are formed here, before the packed loads: formed after
+    // them, hipcc fused r * groups + b / 4 into a 64-bit multiply-add whose (ignored) high
+    // addend was a packed load's destination, so the gathers waited for that load (+1 us).
+    uint32_t ia1 = 0, ia2 = 0;
+    if (shared) {
+        const uint32_t g = min(g0 + lane, gl);
+        const uint32_t r = fdiv(g, A.bpr);
+        const uint32_t b = g - r * A.bpr.d;
+        if constexpr (MODE == kRef) {
+            ia1 = fmodu(g, A.nb);
+            ia2 = fmodu(r * A.groups + (b >> 2), A.n2);
+        } else {
+            ia2 = r * A.rs + b;
+        }
+    }
+    uint32_t w[4], rel[4], col[4], gsel[4];
+    float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    uint32_t ga1 = 0;
+    float ga2 = 0.0f;
+    auto gather = [&]() {
+        if (shared) {
+            if constexpr (MODE == kRef) ga1 = A.a1[ia1];
+            ga2 = A.a2[ia2];
+        }
+    };
+    if constexpr (NF4_DQ_CHUNK_GATHER == 1) gather();
+    if (A.L.d >= 64u) {
+        // Rows of >= 64 chunks (n >= 505): the wave touches at most 6 rows and 38 blocks
+        // (shared scales), and step j+1's chunk is step j's + 64, at most one row further,
+        // so every index advances by additions -- no division or multiply per step.
+        uint32_t q = q0 + lane;
+        bool wrap = q >= A.L.d;
+        q = wrap ? q - A.L.d : q;
+        uint32_t pr = wrap ? A.stride : 0u;          // (r - r0) * stride
+        uint32_t er = wrap ? A.n - 8u * q0 : 0u - 8u * q0;  // (r - r0) * n - 8 q0
+        uint32_t gr = (wrap ? A.bpr.d : 0u) + r0 * A.bpr.d - g0;  // r * bpr - g0
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j) {
+                q += 64u;
+                wrap = q >= A.L.d;
+                q = wrap ? q - A.L.d : q;
+                pr += wrap ? A.stride : 0u;
+                er += wrap ? A.n : 0u;
+                gr += wrap ? A.bpr.d : 0u;
+            }
+            const bool ok = cw + 64u * j + lane < A.chunks;
+            w[j] = load_chunk(ok ? pr + 4u * q : kDrop);
+            col[j] = ok ? 8u * q : 0x7FFFFFF0u;  // past n (< 2^28) for every piece of a chunk past the end
+            rel[j] = er + 8u * q;
+            gsel[j] = gr + (q >> 3);
+        }
+    } else {
+        // (indices first, then the loads, then any per-lane gathers: see ia1 / ia2 above)
+        uint32_t po[4], pa1[4], pa2[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t c = cw + 64u * j + lane;
+            const bool ok = c < A.chunks;
+            const uint32_t r = ok ? fdiv(c, A.L) : r0;
+            const uint32_t q = ok ? c - r * A.L.d : q0;
+            po[j] = ok ? (r - r0) * A.stride + 4u * q : kDrop;
+            col[j] = ok ? 8u * q : 0x7FFFFFF0u;
+            rel[j] = (r - r0) * A.n + 8u * q - 8u * q0;
+            gsel[j] = r * A.bpr.d + (q >> 3) - g0;
+            const uint32_t b = q >> 3;
+            if constexpr (MODE == kRef) {
+                pa1[j] = fmodu(r * A.bpr.d + b, A.nb);
+                pa2[j] = fmodu(r * A.groups + (b >> 2), A.n2);
+            } else {
+                pa1[j] = 0;
+                pa2[j] = r * A.rs + b;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = load_chunk(po[j]);
+        if (!shared) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if constexpr (MODE == kRef) s[j] = ((float)A.a1[pa1[j]] / 127.0f) * A.a2[pa2[j]];
+                else s[j] = A.a2[pa2[j]];
+            }
+        }
+    }
+    if constexpr (NF4_DQ_CHUNK_GATHER == 2) __builtin_amdgcn_s_waitcnt(0xF73);  // vmcnt(3): the first load is back
+    if constexpr (NF4_DQ_CHUNK_GATHER != 1) gather();  // (after the packed loads are out, as in the flat kernel)
+    float sb = 0.0f;
+    if constexpr (MODE == kRef) sb = ((float)ga1 / 127.0f) * ga2;  // IEEE division (:45, :270)
+    else sb = ga2;
+    auto store16 = [&](int j, const uint32_t (&p)[4]) {  // one chunk of 16-bit outputs
+        const uint32_t ob = rel[j] * 2u;
+        if constexpr (SW == 16) {
+            const u32x4 o = {p[0], p[1], p[2], p[3]};
+            __builtin_amdgcn_raw_buffer_store_b128(o, ro, col[j] < A.n ? ob : kDrop, 0, kAuxStore);
+        } else if constexpr (SW == 4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                __builtin_amdgcn_raw_buffer_store_b32(p[k], ro, col[j] + 2u * k < A.n ? ob + 4u * k : kDrop, 0,
+                                                      kAuxPiece);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(p[i >> 1] >> (16 * (i & 1))), ro,
+                                                      col[j] + i < A.n ? ob + 2u * i : kDrop, 0, kAuxPiece);
+        }
+    };
+    if constexpr (DT != NF4DQ_F32) {
+        if (A.L.d >= 64u) {  // every wave of the launch: no workgroup barrier on this path
+            // one table per block of the wave (chunk_table_build / chunk_table_decode)
+            const uint32_t region = (threadIdx.x >> 6) << 11;
+            chunk_table_build<DT>(ctbl, region, lane, sb);
+            if constexpr (NF4_DQ_CHUNK_SYNC) __syncthreads();
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t p[4];
+                chunk_table_decode(ctbl, region, w[j], gsel[j], p);
+                store16(j, p);
+            }
+            return;
+        }
+    }
+    write_lut(lut);
+    __syncthreads();
+    const char* t = reinterpret_cast<const char*>(lut);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t hi4 = (w[j] >> 2) & 0x3C3C3C3Cu;
+        const uint32_t lo4 = (w[j] << 2) & 0x3C3C3C3Cu;
+        const float sh = __shfl(sb, (int)gsel[j], 64);
+        const float sj = shared ? sh : s[j];
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[2 * k] = *reinterpret_cast<const float*>(t + ((hi4 >> (8 * k)) & 0xFFu)) * sj;
+            v[2 * k + 1] = *reinterpret_cast<const float*>(t + ((lo4 >> (8 * k)) & 0xFFu)) * sj;
+        }
+        if constexpr (DT == NF4DQ_F32) {
+            const uint32_t ob = rel[j] * 4u;
+            if constexpr (SW == 16) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const u32x4 o = {__float_as_uint(v[4 * h]), __float_as_uint(v[4 * h + 1]),
+                                     __float_as_uint(v[4 * h + 2]), __float_as_uint(v[4 * h + 3])};
+                    __builtin_amdgcn_raw_buffer_store_b128(o, ro, col[j] + 4u * h < A.n ? ob + 16u * h : kDrop, 0,
+                                                           kAuxStore);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ro, col[j] + i < A.n ? ob + 4u * i : kDrop,
+                                                          0, kAuxPiece);
+            }
+        } else {
+            uint32_t p[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) p[k] = pack2<DT>(v[2 * k], v[2 * k + 1]);
+            store16(j, p);
+        }
     }
 }
 
@@ -734,13 +1083,90 @@ Desc ref_desc(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int6
     return d;
 }
 
+// Fill the chunk kernel's shape fields, or return false when the matrix is past its
+// limits: every index it forms is 32-bit (chunks, blocks, scale indices, offsets within
+// the rows one wave's 256 chunks touch) and its stores need element-aligned output.
+bool chunk_args(ChunkArgs& A, const uint8_t* packed, int64_t packed_len, void* out, int32_t dtype, int64_t m,
+                int64_t n) {
+    const int64_t stride = packed_len / m;
+    const int64_t L = ((n + 1) / 2 + 3) / 4;
+    const int64_t bpr = (n + 63) / 64;
+    const int64_t ob = dtype == NF4DQ_F32 ? 4 : 2;
+    const int64_t span = 256 / L + 2;  // rows one wave touches, at most
+    const int64_t lim = int64_t(1) << 31;
+    if (m * L >= lim - 1024 || m * bpr >= lim || n >= (int64_t(1) << 28) || span * stride >= lim ||
+        span * n * ob >= lim || !aligned(out, (uintptr_t)ob))
+        return false;
+    A.packed = packed;
+    A.out = out;
+    A.packed_len = (uint64_t)packed_len;
+    A.out_elems = (uint64_t)(m * n);
+    A.stride = (uint32_t)stride;
+    A.n = (uint32_t)n;
+    A.chunks = (uint32_t)(m * L);
+    A.L = make_fastdiv((uint32_t)L);
+    A.bpr = make_fastdiv((uint32_t)bpr);
+    A.groups = (uint32_t)((bpr + 3) / 4);
+    return true;
+}
+
+template <int DT, int MODE, int LW>
+void launch_chunks_lw(const ChunkArgs& A, int sw, unsigned g, hipStream_t st) {
+    if (sw == 16) {
+        hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 16>), dim3(g), dim3(kWg), 0, st, A);
+    } else if (DT == NF4DQ_F32 || sw == 4) {
+        hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 4>), dim3(g), dim3(kWg), 0, st, A);
+    } else {
+        if constexpr (DT != NF4DQ_F32)
+            hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 2>), dim3(g), dim3(kWg), 0, st, A);
+    }
+}
+
+template <int MODE>
+int launch_chunks(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
+    const unsigned g = (unsigned)((A.chunks + 1023u) / 1024u);  // 4 waves x 256 chunks
+    if (dtype != NF4DQ_F32 && A.L.d >= 64u && A.stride == 4u * A.L.d && A.n % 8u == 0 && aligned(A.packed, 4) &&
+        aligned(A.out, 16) && A.chunks < (1u << 27)) {
+        if (dtype == NF4DQ_BF16) hipLaunchKernelGGL((nf4_chunk_dense_kernel<NF4DQ_BF16, MODE>), dim3(g), dim3(kWg), 0, st, A);
+        else hipLaunchKernelGGL((nf4_chunk_dense_kernel<NF4DQ_F16, MODE>), dim3(g), dim3(kWg), 0, st, A);
+        return hip_rc(hipGetLastError());
+    }
+    const int lw = aligned(A.packed, 4) && A.stride % 4 == 0 ? 4 : 1;
+    int sw;
+    if (dtype == NF4DQ_F32) sw = A.n % 4 == 0 && aligned(A.out, 16) ? 16 : 4;
+    else sw = A.n % 8 == 0 && aligned(A.out, 16) ? 16 : (A.n % 2 == 0 && aligned(A.out, 4) ? 4 : 2);
+#define NF4_C(DT_)                                                                 \
+    do {                                                                           \
+        if (lw == 4) launch_chunks_lw<DT_, MODE, 4>(A, sw, g, st);                 \
+        else launch_chunks_lw<DT_, MODE, 1>(A, sw, g, st);                         \
+    } while (0)
+    if (dtype == NF4DQ_BF16) NF4_C(NF4DQ_BF16);
+    else if (dtype == NF4DQ_F16) NF4_C(NF4DQ_F16);
+    else NF4_C(NF4DQ_F32);
+#undef NF4_C
+    return hip_rc(hipGetLastError());
+}
+
+inline FastDiv clamped_fastdiv(int64_t d) {  // moduli above 2^31 never wrap for indices < 2^31
+    return make_fastdiv((uint32_t)(d > (int64_t(1) << 31) ? (int64_t(1) << 31) : d));
+}
+
 int ref_impl(const uint8_t* packed, int64_t packed_len, const uint8_t* a1, int64_t nb, const float* a2, int64_t n2,
              void* out, int32_t dtype, int64_t m, int64_t n, const nf4_launch_cfg& cfg, hipStream_t st) {
     int rc = check_common(packed, packed_len, out, dtype, m, n);
     if (rc || m == 0 || n == 0) return rc;
     if (!a1 || !a2 || nb <= 0 || n2 <= 0) return NF4DQ_ERR_ARG;
-    if (flat_eligible(packed, packed_len, out, m, n))
+    const bool rows_only = cfg.flags & NF4DQ_CFG_ROWS, chunks = cfg.flags & NF4DQ_CFG_CHUNKS;
+    if (!rows_only && !chunks && flat_eligible(packed, packed_len, out, m, n))
         return launch_flat_matrix(ref_desc(packed, packed_len, a1, nb, a2, n2, out, n), m, n, dtype, kRef, cfg, st);
+    ChunkArgs C{};
+    if (!rows_only && chunk_args(C, packed, packed_len, out, dtype, m, n)) {
+        C.a1 = a1;
+        C.a2 = a2;
+        C.nb = clamped_fastdiv(nb);
+        C.n2 = clamped_fastdiv(n2);
+        return launch_chunks<kRef>(C, dtype, st);
+    }
     RowsArgs A{};
     A.packed = packed;
     A.a1 = a1;
@@ -777,7 +1203,8 @@ int nf4_dequant_ref_cfg(const uint8_t* packed, int64_t packed_len, const uint8_t
                         const nf4_launch_cfg* cfg, void* hip_stream) {
     nf4_launch_cfg c = cfg ? *cfg : kDefaultCfg;
     if (c.tile_dwords != 4 || c.nontemporal != 1 || c.blocks_per_cu < 0) return NF4DQ_ERR_ARG;
-    if (c.flags != 0) return NF4DQ_ERR_ARG;  // reserved
+    if (c.flags & ~(NF4DQ_CFG_ROWS | NF4DQ_CFG_CHUNKS)) return NF4DQ_ERR_ARG;
+    if ((c.flags & NF4DQ_CFG_ROWS) && (c.flags & NF4DQ_CFG_CHUNKS)) return NF4DQ_ERR_ARG;
     return ref_impl(packed, packed_len, absmax_q, nb, absmax2, n2, out, out_dtype, m, n, c,
                     reinterpret_cast<hipStream_t>(hip_stream));
 }
@@ -795,6 +1222,12 @@ int nf4_dequant_single(const uint8_t* packed, int64_t packed_len, const float* a
         Desc d = ref_desc(packed, packed_len, nullptr, 1, absmax, 1, out, n);
         d.n2 = make_fastdiv((uint32_t)rs);
         return launch_flat_matrix(d, m, n, out_dtype, kSingle, kDefaultCfg, st);
+    }
+    ChunkArgs C{};
+    if (m * rs < (int64_t(1) << 31) && chunk_args(C, packed, packed_len, out, out_dtype, m, n)) {
+        C.a2 = absmax;
+        C.rs = (uint32_t)rs;
+        return launch_chunks<kSingle>(C, out_dtype, st);
     }
     RowsArgs A{};
     A.packed = packed;

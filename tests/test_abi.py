@@ -132,8 +132,10 @@ def test_cfg_validation():
     L = _lib.lib()
     cfg = _lib.LaunchCfg(3, 0, 0, 0)
     assert L.nf4_dequant_ref_cfg(FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, ctypes.byref(cfg), None) == _lib.ERR_ARG
-    # only tile_dwords 4, nontemporal 1 and a grid cap >= 0 remain; flags is reserved and must be 0
-    for bad in ((8, 0, 1, 0), (2, 0, 1, 0), (4, 0, 0, 0), (4, -1, 1, 0), (4, 0, 1, 1), (4, 0, 1, 0x8),
+    # only tile_dwords 4, nontemporal 1 and a grid cap >= 0 remain; flags is 0, NF4DQ_CFG_ROWS or
+    # NF4DQ_CFG_CHUNKS (not both, no other bit)
+    assert (_lib.CFG_ROWS, _lib.CFG_CHUNKS) == (1, 2)
+    for bad in ((8, 0, 1, 0), (2, 0, 1, 0), (4, 0, 0, 0), (4, -1, 1, 0), (4, 0, 1, 3), (4, 0, 1, 4), (4, 0, 1, 0x8),
                 (4, 0, 1, 0x100), (4, 0, 1, 0x2000), (4, 0, 1, 0x10000)):
         cfg = _lib.LaunchCfg(*bad)
         assert L.nf4_dequant_ref_cfg(FAKE, 64, FAKE, 2, FAKE, 1, FAKE, 1, 2, 64, ctypes.byref(cfg), None) == \

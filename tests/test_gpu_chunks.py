@@ -1,0 +1,160 @@
+"""The chunk kernel (``-m gpu``): every shape the flat kernel does not take.
+
+n % 64 != 0, padded packed rows and unaligned pointers go through nf4_chunk_kernel
+(csrc/nf4_dequant.hip).  Its load form (dword / byte) and store form (16-byte chunks,
+4-byte pieces, 2-byte elements) are picked from n, the row stride and the pointer
+alignment; these cases run every combination through the C ABI in both scale modes
+and compare bit for bit with the C oracle, and check that no byte outside the output
+is written (past-n pieces are dropped by the buffer range, not branched around).
+The NF4DQ_CFG_CHUNKS / NF4DQ_CFG_ROWS tuning flags cross-check the chunk kernel
+against the flat kernel and the one-thread-per-byte kernel.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import nf4_oracle as O
+from _helpers import DT_CODE, assert_bits_equal, out_bits
+
+pytestmark = pytest.mark.gpu
+
+TORCH_DT = {"f16": torch.float16, "bf16": torch.bfloat16, "f32": torch.float32}
+GUARD = 64  # elements of sentinel on each side of the output
+
+
+def _lib():
+    from nf4_triton_dequantization_amd import _lib
+
+    return _lib
+
+
+def _dev_bytes(a: np.ndarray, dev, offset=0):
+    """`a` on the device at byte `offset` (0..3) into a fresh allocation, and that allocation."""
+    big = torch.zeros(a.size + 8, dtype=torch.uint8, device=dev)
+    big[offset:offset + a.size] = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
+    return big, big.data_ptr() + offset
+
+
+def _out_buffer(m, n, dt, dev, elem_offset):
+    """An output of m*n elements at `elem_offset` elements into a sentinel-filled buffer."""
+    buf = torch.full((GUARD + elem_offset + m * n + GUARD,), float("nan"), dtype=TORCH_DT[dt], device=dev)
+    bits = buf.view(torch.int32 if dt == "f32" else torch.int16)
+    bits.fill_(0x5A5A5A5A if dt == "f32" else 0x5A5A)
+    return buf, GUARD + elem_offset
+
+
+def _check(buf, start, m, n, dt, want, what):
+    bits = buf.view(torch.int32 if dt == "f32" else torch.int16).cpu().numpy()
+    sentinel = 0x5A5A5A5A if dt == "f32" else 0x5A5A
+    assert (bits[:start] == sentinel).all(), f"{what}: write before the output"
+    assert (bits[start + m * n:] == sentinel).all(), f"{what}: write past the output"
+    got = bits[start:start + m * n].view(np.uint32 if dt == "f32" else np.uint16).reshape(m, n)
+    assert_bits_equal(got, want, dt, what)
+
+
+def _ref_call(dev, p, a1, a2, m, n, dt, p_off=0, o_elem_off=0, flags=None):
+    L = _lib().lib()
+    pb, pp = _dev_bytes(p, dev, p_off)
+    t1 = torch.from_numpy(a1).to(dev)
+    t2 = torch.from_numpy(a2).to(dev)
+    buf, start = _out_buffer(m, n, dt, dev, o_elem_off)
+    optr = buf.data_ptr() + start * buf.element_size()
+    st = torch.cuda.current_stream().cuda_stream
+    if flags is None:
+        rc = L.nf4_dequant_ref(pp, p.size, t1.data_ptr(), t1.numel(), t2.data_ptr(), t2.numel(), optr,
+                               DT_CODE[dt], m, n, st)
+    else:
+        cfg = _lib().LaunchCfg(4, 0, 1, flags)
+        rc = L.nf4_dequant_ref_cfg(pp, p.size, t1.data_ptr(), t1.numel(), t2.data_ptr(), t2.numel(), optr,
+                                   DT_CODE[dt], m, n, ctypes.byref(cfg), st)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    del pb
+    return buf, start
+
+
+# (m, n, extra stride bytes, packed byte offset, output element offset): the forms they select
+CASES = [
+    (37, 1000, 0, 0, 0),      # n % 8 == 0, dense rows >= 64 chunks: the dense form
+    (5, 4080, 0, 0, 0),
+    (33, 1000, 4, 0, 0),      # padded rows of >= 64 chunks: dword loads, 16-byte chunk stores
+    (9, 4080, 0, 0, 1),       # output off 16-byte alignment: 4-byte pieces
+    (9, 1002, 0, 0, 0),       # n % 8 == 2: 4-byte pieces (16-bit) / 4-byte elements (fp32)
+    (3, 6, 0, 0, 0),
+    (7, 77, 0, 0, 0),         # odd n: 2-byte elements, byte loads (stride 39)
+    (1, 1, 0, 0, 0),
+    (4, 3, 0, 0, 0),
+    (11, 200, 3, 0, 0),       # padded rows, stride % 4 != 0: byte loads
+    (11, 200, 4, 0, 0),       # padded rows, stride % 4 == 0: dword loads
+    (6, 256, 2, 0, 0),        # n % 64 == 0 but padded: not flat
+    (6, 256, 0, 1, 0),        # odd packed pointer
+    (6, 256, 0, 2, 1),        # output one element off 16-byte alignment
+    (10, 1000, 0, 3, 3),
+    (3000, 2, 0, 0, 0),       # one chunk per row: 256 rows per wave
+    (300, 18, 5, 0, 1),
+    (129, 4100, 0, 0, 0),     # partial last wave
+]
+
+
+@pytest.mark.parametrize("dt", ["f16", "bf16", "f32"])
+@pytest.mark.parametrize("m,n,pad,poff,ooff", CASES)
+def test_chunk_kernel_forms_vs_oracle(coracle, gpu, dt, m, n, pad, poff, ooff):
+    seed = 31 * m + n + pad + 7 * poff + 3 * ooff
+    for ov in ({}, {"nb": 5, "n2": 3, "a2_kind": "normal"}):
+        stride = (n + 1) // 2 + pad
+        p, a1, a2, _ = O.golden_case_inputs(m, n, seed, dict(ov, stride=stride))
+        want = coracle.dequant_ref(p, a1, a2, m, n, DT_CODE[dt])
+        buf, start = _ref_call(gpu, p, a1, a2, m, n, dt, poff, ooff)
+        _check(buf, start, m, n, dt, want, f"{m}x{n} pad {pad} poff {poff} ooff {ooff} {dt} {ov}")
+
+
+@pytest.mark.parametrize("dt", ["f16", "bf16", "f32"])
+def test_single_quant_chunk_kernel(coracle, gpu, dt):
+    L = _lib().lib()
+    for (m, n, extra, pad) in ((12, 200, 0, 0), (6, 1002, 3, 1), (33, 77, 1, 0), (5, 4080, 2, 4)):
+        stride = (n + 1) // 2 + pad
+        p, _, _, single = O.golden_case_inputs(m, n, m + n, {"single": extra, "stride": stride})
+        want = coracle.dequant_single(p, single, m, n, DT_CODE[dt])
+        pb, pp = _dev_bytes(p, gpu)
+        ts = torch.from_numpy(single).to(gpu)
+        buf, start = _out_buffer(m, n, dt, gpu, 0)
+        rc = L.nf4_dequant_single(pp, p.size, ts.data_ptr(), ts.numel(), buf.data_ptr() + start * buf.element_size(),
+                                  DT_CODE[dt], m, n, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        _check(buf, start, m, n, dt, want, f"single {m}x{n} pad {pad} {dt}")
+
+
+@pytest.mark.parametrize("m,n", [(256, 1024), (1000, 4096), (7, 64)])
+def test_chunk_kernel_equals_flat_kernel_on_flat_shapes(coracle, gpu, m, n):
+    """NF4DQ_CFG_CHUNKS sends a flat-eligible matrix through the chunk kernel."""
+    p, a1, a2, _ = O.golden_case_inputs(m, n, 900 + m, {"a2_kind": "normal"})
+    want = coracle.dequant_ref(p, a1, a2, m, n, O.BF16)
+    for flags in (0, _lib().CFG_CHUNKS, _lib().CFG_ROWS):
+        buf, start = _ref_call(gpu, p, a1, a2, m, n, "bf16", flags=flags)
+        _check(buf, start, m, n, "bf16", want, f"{m}x{n} flags {flags}")
+
+
+@pytest.mark.parametrize("dt", ["f16", "f32"])
+def test_rows_kernel_still_matches(coracle, gpu, dt):
+    """NF4DQ_CFG_ROWS: the one-thread-per-byte kernel (past the chunk kernel's limits)."""
+    for (m, n, pad) in ((9, 1002, 0), (7, 77, 0), (11, 200, 3)):
+        p, a1, a2, _ = O.golden_case_inputs(m, n, m * n, {"stride": (n + 1) // 2 + pad, "nb": 11, "n2": 2})
+        want = coracle.dequant_ref(p, a1, a2, m, n, DT_CODE[dt])
+        buf, start = _ref_call(gpu, p, a1, a2, m, n, dt, flags=_lib().CFG_ROWS)
+        _check(buf, start, m, n, dt, want, f"rows {m}x{n} {dt}")
+
+
+def test_drop_in_takes_the_chunk_kernel_for_odd_widths(coracle, gpu):
+    """The drop-in API on a BASELINE-sized matrix with n % 64 != 0."""
+    import nf4_triton_dequantization as N
+    from _helpers import make_module
+
+    m, n = 4096, 4080
+    p, a1, a2, _ = O.golden_case_inputs(m, n, 4080, {"stride": n // 2})
+    want = coracle.dequant_ref(p, a1, a2, m, n, O.BF16)
+    out = N.triton_dequantize_nf4(make_module(p, a1, a2, m, n, "bf16", gpu))
+    assert out.shape == (m, n) and out.is_contiguous()
+    assert_bits_equal(out_bits(out), want, "bf16", "drop-in 4096x4080")

@@ -77,7 +77,7 @@ def test_random_shapes_vs_c_oracle(coracle, gpu, m, n, dt):
 
 
 def test_padded_rows_and_unaligned_views(coracle, gpu):
-    """Row stride > n/2 and a packed view at an odd byte offset take the rows kernel."""
+    """Row stride > n/2 and a packed view at an odd byte offset take the chunk kernel."""
     m, n = 6, 256
     p, a1, a2, _ = O.golden_case_inputs(m, n, 5, {"stride": 130})
     want = coracle.dequant_ref(p, a1, a2, m, n, O.BF16)
@@ -181,7 +181,7 @@ def test_batched_matches_single_calls(coracle, gpu):
 
 # the one launch knob the library keeps (include/nf4_dequant.h): the grid cap
 # (persistent waves walking several tiles; 1 and 3 workgroups per CU give odd and
-# even tile counts, so both loop exits run); flags is reserved (0)
+# even tile counts, so both loop exits run); flags 0 (the kernel-choice flags: test_gpu_chunks.py)
 @pytest.mark.parametrize("cfg", [(4, 0, 1, 0), (4, 1, 1, 0), (4, 2, 1, 0), (4, 3, 1, 0), (4, 8, 1, 0)])
 def test_launch_configs_identical(coracle, gpu, cfg):
     from nf4_triton_dequantization_amd import _lib

@@ -1,0 +1,132 @@
+"""The chunk kernel against the flat kernel, HBM-streamed, interleaved rounds (tools only).
+
+    python tools/chunk_ab.py [--rounds 7] [--steps 64]
+
+Cases (bf16, bench.py's rotation: >= 512 MiB of distinct reads and of writes; eager
+launches behind a spin, as bench.py times its steps):
+  flat_4096     4096x4096 through the default path (the flat kernel)
+  chunk_4096    the same matrices through the chunk kernel (nf4_dequant_ref_cfg flags =
+                NF4DQ_CFG_CHUNKS): the kernel's own cost on the flat kernel's stream
+  chunk_4080    4096x4080 (n % 64 != 0): the chunk kernel, as the drop-in runs it
+  rows_4080     4096x4080 through the one-thread-per-byte kernel (NF4DQ_CFG_ROWS)
+  chunk_4095    4096x4095 (odd n: 2-byte stores)
+  chunk_4090    4096x4090 (n % 8 == 2: 4-byte stores)
+--libs a,b: the same cases through other builds of the library (tools/_build/libnf4dq_<x>.so),
+interleaved, tagged "<x>:<case>".
+Prints one JSON line per case: median / min / max us per launch and the fraction of
+8 TB/s (SURVEY §8d algorithmic bytes).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tools"))
+from nf4_triton_dequantization_amd import _lib  # noqa: E402
+from bench_configs import PEAK, alg_bytes, rotating_sets, rotation  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--cases", default="flat_4096,chunk_4096,chunk_4080,rows_4080,chunk_4095,chunk_4090")
+    ap.add_argument("--libs", default="")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    libs = {"prod": _lib.lib()}
+    for path in [v for v in args.libs.split(",") if v]:
+        h = ctypes.CDLL(os.path.abspath(path))
+        for fname, (res_t, argt) in _lib.SIGNATURES.items():
+            fn = getattr(h, fname, None)
+            if fn is not None:
+                fn.restype, fn.argtypes = res_t, argt
+        libs[os.path.basename(path).replace("libnf4dq_", "").replace(".so", "")] = h
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    torch.cuda._sleep(2_000_000)
+    e1.record(st)
+    torch.cuda.synchronize()
+    cyc_per_us = 2_000_000 / max(e0.elapsed_time(e1) * 1e3, 1.0)
+    shapes = {"flat_4096": (4096, 4096, 0), "chunk_4096": (4096, 4096, _lib.CFG_CHUNKS),
+              "chunk_4080": (4096, 4080, 0), "rows_4080": (4096, 4080, _lib.CFG_ROWS),
+              "chunk_4095": (4096, 4095, 0), "chunk_4090": (4096, 4090, 0)}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(3)
+    sets = {}
+    for name in args.cases.split(","):
+        m, n, flags = shapes[name]
+        key = (m, n)
+        if key not in sets:
+            pin, pout = rotation(m, n, 2)
+            if n % 2:  # odd n: packed rows of ceil(n/2) bytes
+                ins = []
+                for _ in range(pin):
+                    nb = m * n // 64 + 1
+                    ins.append((torch.randint(0, 256, (m * ((n + 1) // 2),), dtype=torch.uint8, device=dev, generator=gen),
+                                torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen),
+                                torch.rand((nb + 255) // 256, device=dev, generator=gen) * 0.01 + 1e-3))
+                outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(pout)]
+            else:
+                ins, outs = rotating_sets(m, n, torch.bfloat16, dev, gen, pin, pout)
+            sets[key] = (ins, outs)
+    cfgs = {f: _lib.LaunchCfg(4, 0, 1, f) for f in (_lib.CFG_CHUNKS, _lib.CFG_ROWS)}
+
+    def launcher(tag):
+        lname, name = tag.split(":")
+        L = libs[lname]
+        m, n, flags = shapes[name]
+        ins, outs = sets[(m, n)]
+
+        def launch(i):
+            q, a1, a2 = ins[i % len(ins)]
+            o = outs[i % len(outs)]
+            if flags:
+                rc = L.nf4_dequant_ref_cfg(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(),
+                                           a2.numel(), o.data_ptr(), _lib.BF16, m, n, ctypes.byref(cfgs[flags]),
+                                           st.cuda_stream)
+            else:
+                rc = L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
+                                       o.data_ptr(), _lib.BF16, m, n, st.cuda_stream)
+            assert rc == 0, rc
+        return launch
+
+    names = [f"{lib}:{c}" for c in args.cases.split(",") for lib in libs]
+    fns = {nm: launcher(nm) for nm in names}
+    for nm in names:  # every set touched once
+        ins, outs = sets[shapes[nm.split(":")[1]][:2]]
+        for i in range(max(len(ins), len(outs))):
+            fns[nm](i)
+    torch.cuda.synchronize()
+    res = {nm: [] for nm in names}
+    for _ in range(args.rounds):
+        for nm in names:
+            torch.cuda._sleep(int(cyc_per_us * (40.0 * (args.steps + 8) + 200.0)))
+            for j in range(8):
+                fns[nm](j - 8)
+            e0.record(st)
+            for i in range(args.steps):
+                fns[nm](i)
+            e1.record(st)
+            torch.cuda.synchronize()
+            res[nm].append(e0.elapsed_time(e1) * 1e3 / args.steps)
+    for nm in names:
+        m, n, flags = shapes[nm.split(":")[1]]
+        ts = sorted(res[nm])
+        med = ts[len(ts) // 2]
+        byt = alg_bytes(m, n, 2)
+        print(json.dumps({"case": nm, "m": m, "n": n, "flags": flags, "steps": args.steps, "rounds": args.rounds,
+                          "us_median": round(med, 3), "us_min": round(ts[0], 3), "us_max": round(ts[-1], 3),
+                          "frac": round(byt / (med * 1e-6) / PEAK, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

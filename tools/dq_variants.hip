@@ -19,6 +19,9 @@
 // delays (at 99ed841).
 //   DQV_SINGLE=1   one-tile waves skip the pipelined loop
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
+//   DQV_CSYNC=1  the chunk kernel's table path with a workgroup barrier after the tables
+//   DQV_CGATHER=n  the chunk kernel's scale gathers: 0 after the packed loads, 1 before them,
+//                  2 after the first packed load is back
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
 #endif
@@ -46,6 +49,12 @@
 #endif
 #ifdef DQV_DEC
 #define NF4_DQ_DECODE DQV_DEC
+#endif
+#ifdef DQV_CSYNC
+#define NF4_DQ_CHUNK_SYNC DQV_CSYNC
+#endif
+#ifdef DQV_CGATHER
+#define NF4_DQ_CHUNK_GATHER DQV_CGATHER
 #endif
 
 #include "../nf4_triton_dequantization_amd/csrc/nf4_dequant.hip"
