@@ -32,8 +32,10 @@
 //    walk several tiles in the software-pipelined loop.
 //  * batched: up to NF4DQ_BATCH_MAX matrices per launch in the kernel
 //    arguments; a wave finds its matrix by scanning scalar tile offsets.
-//  * "rows" kernels: any other shape (partial blocks, padded rows, odd n) --
-//    one thread per packed byte, 64-bit indexing, same arithmetic.
+//  * "chunk" kernels: any other shape (partial blocks, padded rows, odd n,
+//    unaligned pointers) -- the flat tile with rows cut out of the stream and
+//    one LDS table per scale block of the wave; the one-thread-per-byte "rows"
+//    kernel only past their 32-bit index limits.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -537,19 +539,27 @@ __global__ __launch_bounds__(kWg) void nf4_rows_kernel(const RowsArgs A) {
     }
 }
 
-// The chunk kernel (round 5): every shape the flat kernel does not take -- n % 64 != 0
+// The chunk kernels (round 5): every shape the flat kernel does not take -- n % 64 != 0
 // (rows end in a partial 64-column block), padded rows, unaligned pointers -- with
 // reference / single-quant semantics.  Each row's packed bytes are cut into 4-byte
 // chunks (L = ceil(ceil(n/2) / 4) per row); chunk c = r * L + q holds columns 8q .. 8q+7
 // of row r, all inside 64-column block q / 8.  A wave owns 256 consecutive chunks, lane l
-// chunk 64 j + l at step j -- the flat kernel's tile with rows cut out of the stream: each
-// load instruction walks a row's bytes contiguously, and when n % 8 == 0 the output of
-// the wave is the dense range 8c .. 8c+7 of 16-byte stores, as in the flat kernel.  Blocks
-// no longer line up with groups of 8 lanes: each lane fetches its block's scale from the
-// lane that gathered it (below) and decodes per nibble.  Partial chunks (n % 8 != 0) store 4- or 2-byte pieces, each past-n
-// piece sent out of the buffer range (dropped) instead of branched around.  The buffer
-// bases are the wave's first row / output element (scalar 64-bit), so only the offsets
-// within one wave's span are 32-bit.
+// chunk 64 j + l at step j -- the flat kernel's tile with rows cut out of the stream.
+// Blocks no longer line up with groups of 8 lanes, but the wave's blocks are consecutive
+// (block g = r * bpr + q / 8 steps by one per 8 chunks, and from a row's last block to the
+// next row's first): lane i gathers block g0 + i's scale and rounds its 16 outputs into a
+// table of the wave's (one per block), and every output is a table lookup.
+//  * nf4_chunk_dense_kernel: 16-bit output, n % 8 == 0 and packed rows of exactly 4 L
+//    bytes (the usual odd-width weight): chunk c is packed bytes 4c.. and output elements
+//    8c.., the flat kernel's stream, so loads and stores need no row arithmetic.
+//    4096 x 4080 bf16: 7.49 us = 70 % of 8 TB/s (flat 4096^2 7.36 on the same box; the
+//    per-byte kernel 33.5), profiles/r05/chunk/s37_chunk_ab_dense_form.jsonl.
+//  * nf4_chunk_kernel: the rest.  The buffer bases are the wave's first row / output
+//    element (scalar 64-bit), so only offsets within one wave's span are 32-bit; rows of
+//    >= 64 chunks advance their indices by additions, shorter rows divide per step (and
+//    gather per lane when the wave spans more than 64 blocks).  Partial chunks (n % 8 !=
+//    0) store 4- or 2-byte pieces, each past-n piece sent out of the buffer range
+//    (dropped) instead of branched around: 20.8 / 28.6 us at 4096 x 4090 / 4095.
 struct ChunkArgs {
     const uint8_t* packed;
     const uint8_t* a1;
@@ -572,12 +582,6 @@ constexpr uint32_t kDrop = 0xFFFFFFF0u;  // an offset past every range: load 0 /
 // of its 1 KiB span) use the default policy, so that the L2 merges a line's pieces before
 // it goes to HBM: streamed (nt) partial-line writes made odd-n matrices 16x slower.
 constexpr int kAuxPiece = 0;
-#ifndef NF4_DQ_CHUNK_SYNC
-#define NF4_DQ_CHUNK_SYNC 0
-#endif
-#ifndef NF4_DQ_CHUNK_GATHER
-#define NF4_DQ_CHUNK_GATHER 0
-#endif
 
 inline __device__ uint32_t range32(uint64_t v) { return v > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)v; }
 
@@ -747,7 +751,6 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             ga2 = A.a2[ia2];
         }
     };
-    if constexpr (NF4_DQ_CHUNK_GATHER == 1) gather();
     if (A.L.d >= 64u) {
         // Rows of >= 64 chunks (n >= 505): the wave touches at most 6 rows and 38 blocks
         // (shared scales), and step j+1's chunk is step j's + 64, at most one row further,
@@ -806,8 +809,7 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             }
         }
     }
-    if constexpr (NF4_DQ_CHUNK_GATHER == 2) __builtin_amdgcn_s_waitcnt(0xF73);  // vmcnt(3): the first load is back
-    if constexpr (NF4_DQ_CHUNK_GATHER != 1) gather();  // (after the packed loads are out, as in the flat kernel)
+    gather();  // (after the packed loads are out, as in the flat kernel)
     float sb = 0.0f;
     if constexpr (MODE == kRef) sb = ((float)ga1 / 127.0f) * ga2;  // IEEE division (:45, :270)
     else sb = ga2;
@@ -833,7 +835,6 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             // one table per block of the wave (chunk_table_build / chunk_table_decode)
             const uint32_t region = (threadIdx.x >> 6) << 11;
             chunk_table_build<DT>(ctbl, region, lane, sb);
-            if constexpr (NF4_DQ_CHUNK_SYNC) __syncthreads();
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 uint32_t p[4];

@@ -15,8 +15,8 @@ c5   one 8192x8192 NF4->bf16 matrix (the per-GPU unit of the 8-GPU config), the 
      rotation and method.
 big  128256x8192 NF4->bf16 (Llama-3-70B lm_head size: 525 MB packed, past one buffer
      descriptor -- two row pieces in one launch).
-rows 4096x4080 NF4->bf16: n % 64 != 0 (every row ends in a partial 64-block), so the
-     matrix takes the general nf4_rows_kernel, not the flat kernel; same method as c4.
+odd  4096x4080 NF4->bf16: n % 64 != 0 (every row ends in a partial 64-block), so the
+     matrix takes the chunk kernel (its dense form), not the flat kernel; same method as c4.
 bnb  4096x4096 NF4->bf16 with bitsandbytes semantics (nf4_dequant_bnb: code2[A1] * A2
      + offset, flat blocks), same method as c4; its algorithmic bytes
      add the 1 KiB nested code book.
@@ -265,7 +265,7 @@ def run_bnb(name, m, n, reps, dev, steps=64):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c3,c3b,c4,c5,big,bnb")
+    ap.add_argument("--configs", default="c3,c3b,c4,c5,big,odd,bnb")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--layers", type=int, default=32)
     args = ap.parse_args()
@@ -292,8 +292,8 @@ def main():
         print(json.dumps(run_single("big 128256x8192 (a 70B lm_head: two flat pieces, one launch)", 128256, 8192,
                                     torch.bfloat16, _lib.BF16, args.reps, dev, steps=8)), flush=True)
         torch.cuda.empty_cache()
-    if "rows" in todo:
-        print(json.dumps(run_single("rows 4096x4080 (n % 64 != 0: the general kernel)", 4096, 4080, torch.bfloat16,
+    if "odd" in todo:
+        print(json.dumps(run_single("odd 4096x4080 (n % 64 != 0: the chunk kernel)", 4096, 4080, torch.bfloat16,
                                     _lib.BF16, args.reps, dev)), flush=True)
         torch.cuda.empty_cache()
     if "bnb" in todo:

@@ -16,12 +16,9 @@
 // without the code table and its barrier, and synchronised stores through hooks removed
 // after measurement (profiles/r05/; the hooks are in git history at 914c6b8), and scale-index shortcuts and
 // gather delays (at 414c083), bitsandbytes-mode code-table loads and gather
-// delays (at 99ed841).
+// delays (at 99ed841), and the chunk kernel's barrier / scale-gather placements (at 1601634).
 //   DQV_SINGLE=1   one-tile waves skip the pipelined loop
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
-//   DQV_CSYNC=1  the chunk kernel's table path with a workgroup barrier after the tables
-//   DQV_CGATHER=n  the chunk kernel's scale gathers: 0 after the packed loads, 1 before them,
-//                  2 after the first packed load is back
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
 #endif
@@ -49,12 +46,6 @@
 #endif
 #ifdef DQV_DEC
 #define NF4_DQ_DECODE DQV_DEC
-#endif
-#ifdef DQV_CSYNC
-#define NF4_DQ_CHUNK_SYNC DQV_CSYNC
-#endif
-#ifdef DQV_CGATHER
-#define NF4_DQ_CHUNK_GATHER DQV_CGATHER
 #endif
 
 #include "../nf4_triton_dequantization_amd/csrc/nf4_dequant.hip"
