@@ -582,8 +582,21 @@ constexpr uint32_t kDrop = 0xFFFFFFF0u;  // an offset past every range: load 0 /
 // of its 1 KiB span) use the default policy, so that the L2 merges a line's pieces before
 // it goes to HBM: streamed (nt) partial-line writes made odd-n matrices 16x slower.
 constexpr int kAuxPiece = 0;
+// A wave's staged 16-bit span: 2048 elements + 7 of misalignment, then one dummy element
+// (past-n elements of a partial chunk), rounded to 16 bytes.
+constexpr uint32_t kStageBytes = 4128;
+constexpr uint32_t kStageDummy = 4112;
 
 inline __device__ uint32_t range32(uint64_t v) { return v > 0x7FFFFFFFull ? 0x7FFFFFFFu : (uint32_t)v; }
+
+// a * b kept apart from the add that follows it: fused, hipcc emits a 64-bit multiply-add
+// whose (ignored) high addend can be any register -- once a packed load's destination, so
+// the scale gathers waited for that load (+1 us per launch).
+inline __device__ uint32_t opaque_mul(uint32_t a, uint32_t b) {
+    uint32_t r = a * b;
+    asm("" : "+v"(r));
+    return r;
+}
 
 // Block-table decode of one wave's 4 steps (16-bit output): lane i has rounded the 16
 // outputs of block g0 + i (fp32 products and RNE, as everywhere) into 32 bytes at the
@@ -654,9 +667,9 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_dense_kernel(const ChunkArgs A)
         const uint32_t b = g - r * A.bpr.d;
         if constexpr (MODE == kRef) {
             const float q8 = (float)A.a1[fmodu(g, A.nb)];
-            sb = (q8 / 127.0f) * A.a2[fmodu(r * A.groups + (b >> 2), A.n2)];  // IEEE division (:45, :270)
+            sb = (q8 / 127.0f) * A.a2[fmodu(opaque_mul(r, A.groups) + (b >> 2), A.n2)];  // IEEE division (:45, :270)
         } else {
-            sb = A.a2[r * A.rs + b];
+            sb = A.a2[opaque_mul(r, A.rs) + b];
         }
     }
     uint32_t gsel[4];
@@ -695,6 +708,7 @@ template <int DT, int MODE, int LW, int SW>
 __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     __shared__ __attribute__((aligned(16))) float lut[16];
     __shared__ __attribute__((aligned(256))) char ctbl[DT == NF4DQ_F32 ? 4 : 4 * 2048];  // 64 block tables per wave
+    __shared__ __attribute__((aligned(16))) char stage[DT != NF4DQ_F32 && SW != 16 ? 4 * kStageBytes : 16];
     constexpr uint32_t kOB = DT == NF4DQ_F32 ? 4u : 2u;  // output bytes per element
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t cw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
@@ -726,29 +740,21 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     const uint32_t g0 = r0 * A.bpr.d + (q0 >> 3);
     const uint32_t gl = rl * A.bpr.d + ((cl - rl * A.L.d) >> 3);
     const bool shared = gl - g0 < 64u;
-    // The shared gathers' indices are formed here, before the packed loads: formed after
-    // them, hipcc fused r * groups + b / 4 into a 64-bit multiply-add whose (ignored) high
-    // addend was a packed load's destination, so the gathers waited for that load (+1 us).
-    uint32_t ia1 = 0, ia2 = 0;
-    if (shared) {
-        const uint32_t g = min(g0 + lane, gl);
-        const uint32_t r = fdiv(g, A.bpr);
-        const uint32_t b = g - r * A.bpr.d;
-        if constexpr (MODE == kRef) {
-            ia1 = fmodu(g, A.nb);
-            ia2 = fmodu(r * A.groups + (b >> 2), A.n2);
-        } else {
-            ia2 = r * A.rs + b;
-        }
-    }
     uint32_t w[4], rel[4], col[4], gsel[4];
     float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t ga1 = 0;
     float ga2 = 0.0f;
-    auto gather = [&]() {
+    auto gather = [&]() {  // (after the packed loads are out, as in the flat kernel)
         if (shared) {
-            if constexpr (MODE == kRef) ga1 = A.a1[ia1];
-            ga2 = A.a2[ia2];
+            const uint32_t g = min(g0 + lane, gl);
+            const uint32_t r = fdiv(g, A.bpr);
+            const uint32_t b = g - r * A.bpr.d;
+            if constexpr (MODE == kRef) {
+                ga1 = A.a1[fmodu(g, A.nb)];
+                ga2 = A.a2[fmodu(opaque_mul(r, A.groups) + (b >> 2), A.n2)];
+            } else {
+                ga2 = A.a2[opaque_mul(r, A.rs) + b];
+            }
         }
     };
     if (A.L.d >= 64u) {
@@ -777,8 +783,9 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             rel[j] = er + 8u * q;
             gsel[j] = gr + (q >> 3);
         }
+        __builtin_amdgcn_sched_barrier(0);  // (keeps the scale gathers behind the loads)
     } else {
-        // (indices first, then the loads, then any per-lane gathers: see ia1 / ia2 above)
+        // (indices first, then the loads, then any per-lane gathers; see opaque_mul)
         uint32_t po[4], pa1[4], pa2[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -793,14 +800,15 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             const uint32_t b = q >> 3;
             if constexpr (MODE == kRef) {
                 pa1[j] = fmodu(r * A.bpr.d + b, A.nb);
-                pa2[j] = fmodu(r * A.groups + (b >> 2), A.n2);
+                pa2[j] = fmodu(opaque_mul(r, A.groups) + (b >> 2), A.n2);
             } else {
                 pa1[j] = 0;
-                pa2[j] = r * A.rs + b;
+                pa2[j] = opaque_mul(r, A.rs) + b;
             }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) w[j] = load_chunk(po[j]);
+        __builtin_amdgcn_sched_barrier(0);
         if (!shared) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -813,21 +821,51 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     float sb = 0.0f;
     if constexpr (MODE == kRef) sb = ((float)ga1 / 127.0f) * ga2;  // IEEE division (:45, :270)
     else sb = ga2;
+    // Narrow 16-bit outputs (n % 8 != 0, or the output off 16-byte alignment) go through
+    // LDS.  The wave's outputs are one contiguous span of the output (a row's last, partial
+    // chunk is followed by the next row's first), so each lane drops its chunk's valid
+    // elements into a copy of the span shifted by the output's misalignment `sa`, and the
+    // wave then writes the span as 16-byte pieces aligned in the output: whole pieces with
+    // one 16-byte store each, the (at most two) pieces at the span's ends element by element,
+    // since a neighbouring wave owns the rest of them.  (Storing 4- or 2-byte pieces
+    // straight from the lanes took 20.8 / 28.6 us at 4096 x 4090 / 4095.)
+    const uint32_t sbase = (threadIdx.x >> 6) * kStageBytes;
+    const uint32_t sa = (uint32_t)(((uintptr_t)A.out >> 1) + e0) & 7u;
     auto store16 = [&](int j, const uint32_t (&p)[4]) {  // one chunk of 16-bit outputs
-        const uint32_t ob = rel[j] * 2u;
         if constexpr (SW == 16) {
             const u32x4 o = {p[0], p[1], p[2], p[3]};
-            __builtin_amdgcn_raw_buffer_store_b128(o, ro, col[j] < A.n ? ob : kDrop, 0, kAuxStore);
-        } else if constexpr (SW == 4) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                __builtin_amdgcn_raw_buffer_store_b32(p[k], ro, col[j] + 2u * k < A.n ? ob + 4u * k : kDrop, 0,
-                                                      kAuxPiece);
+            __builtin_amdgcn_raw_buffer_store_b128(o, ro, col[j] < A.n ? rel[j] * 2u : kDrop, 0, kAuxStore);
         } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(p[i >> 1] >> (16 * (i & 1))), ro,
-                                                      col[j] + i < A.n ? ob + 2u * i : kDrop, 0, kAuxPiece);
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t off = col[j] + i < A.n ? 2u * (rel[j] + i + sa) : kStageDummy;
+                *reinterpret_cast<u16_alias*>(stage + sbase + off) = (uint16_t)(p[i >> 1] >> (16 * (i & 1)));
+            }
+        }
+    };
+    auto flush16 = [&]() {
+        if constexpr (SW != 16) {
+            const uint32_t cl2 = min(cw + 255u, A.chunks - 1u);
+            const uint32_t rl2 = fdiv(cl2, A.L);
+            const uint32_t ql2 = cl2 - rl2 * A.L.d;
+            const uint32_t span = (uint32_t)((uint64_t)rl2 * A.n + min(8u * ql2 + 8u, A.n) - e0);
+#pragma unroll
+            for (int st = 0; st < 5; ++st) {
+                const int x0 = (int)(8u * (lane + 64u * st)) - (int)sa;  // piece k = lane + 64 st
+                if (x0 >= (int)span) break;
+                const bool whole = x0 >= 0 && x0 + 8 <= (int)span;
+                const u32x4 v = *reinterpret_cast<const u32x4_alias*>(stage + sbase + 16u * (lane + 64u * st));
+                __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxStore);
+                if (!whole) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int x = x0 + i;
+                        const uint16_t e = (uint16_t)(v[i >> 1] >> (16 * (i & 1)));
+                        __builtin_amdgcn_raw_buffer_store_b16(e, ro, x >= 0 && x < (int)span ? 2u * (uint32_t)x : kDrop, 0,
+                                                              kAuxPiece);
+                    }
+                }
+            }
         }
     };
     if constexpr (DT != NF4DQ_F32) {
@@ -841,6 +879,7 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
                 chunk_table_decode(ctbl, region, w[j], gsel[j], p);
                 store16(j, p);
             }
+            flush16();
             return;
         }
     }
@@ -882,6 +921,7 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             store16(j, p);
         }
     }
+    if constexpr (DT != NF4DQ_F32) flush16();
 }
 
 // Any length, bitsandbytes semantics: one thread per packed byte.

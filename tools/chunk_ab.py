@@ -11,6 +11,8 @@ launches behind a spin, as bench.py times its steps):
   rows_4080     4096x4080 through the one-thread-per-byte kernel (NF4DQ_CFG_ROWS)
   chunk_4095    4096x4095 (odd n: 2-byte stores)
   chunk_4090    4096x4090 (n % 8 == 2: 4-byte stores)
+  pad_4096      4096x4096 with packed rows of 2052 bytes (the general form, dword loads)
+  unal_4096     4096x4096 with the packed weight at an odd address (byte loads)
 --libs a,b: the same cases through other builds of the library (tools/_build/libnf4dq_<x>.so),
 interleaved, tagged "<x>:<case>".
 Prints one JSON line per case: median / min / max us per launch and the fraction of
@@ -58,20 +60,27 @@ def main():
     cyc_per_us = 2_000_000 / max(e0.elapsed_time(e1) * 1e3, 1.0)
     shapes = {"flat_4096": (4096, 4096, 0), "chunk_4096": (4096, 4096, _lib.CFG_CHUNKS),
               "chunk_4080": (4096, 4080, 0), "rows_4080": (4096, 4080, _lib.CFG_ROWS),
-              "chunk_4095": (4096, 4095, 0), "chunk_4090": (4096, 4090, 0)}
+              "chunk_4095": (4096, 4095, 0), "chunk_4090": (4096, 4090, 0),
+              "pad_4096": (4096, 4096, 0), "unal_4096": (4096, 4096, 0)}
+    # pad_4096: packed rows of 2052 bytes (n % 64 == 0 but not dense: the general form with
+    # dword loads); unal_4096: the packed weight one byte into its allocation (byte loads)
+    pad = {"pad_4096": 4}
+    unal = {"unal_4096": 1}
     gen = torch.Generator(device=dev)
     gen.manual_seed(3)
     sets = {}
     for name in args.cases.split(","):
         m, n, flags = shapes[name]
-        key = (m, n)
+        key = (m, n, pad.get(name, 0), unal.get(name, 0))
         if key not in sets:
             pin, pout = rotation(m, n, 2)
-            if n % 2:  # odd n: packed rows of ceil(n/2) bytes
+            if n % 2 or key[2] or key[3]:  # packed rows of ceil(n/2) + pad bytes, at byte offset unal
                 ins = []
+                stride = (n + 1) // 2 + key[2]
                 for _ in range(pin):
                     nb = m * n // 64 + 1
-                    ins.append((torch.randint(0, 256, (m * ((n + 1) // 2),), dtype=torch.uint8, device=dev, generator=gen),
+                    q = torch.randint(0, 256, (m * stride + key[3],), dtype=torch.uint8, device=dev, generator=gen)
+                    ins.append((q[key[3]:],
                                 torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen),
                                 torch.rand((nb + 255) // 256, device=dev, generator=gen) * 0.01 + 1e-3))
                 outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(pout)]
@@ -84,7 +93,7 @@ def main():
         lname, name = tag.split(":")
         L = libs[lname]
         m, n, flags = shapes[name]
-        ins, outs = sets[(m, n)]
+        ins, outs = sets[(m, n, pad.get(name, 0), unal.get(name, 0))]
 
         def launch(i):
             q, a1, a2 = ins[i % len(ins)]
@@ -102,7 +111,8 @@ def main():
     names = [f"{lib}:{c}" for c in args.cases.split(",") for lib in libs]
     fns = {nm: launcher(nm) for nm in names}
     for nm in names:  # every set touched once
-        ins, outs = sets[shapes[nm.split(":")[1]][:2]]
+        c = nm.split(":")[1]
+        ins, outs = sets[shapes[c][:2] + (pad.get(c, 0), unal.get(c, 0))]
         for i in range(max(len(ins), len(outs))):
             fns[nm](i)
     torch.cuda.synchronize()
