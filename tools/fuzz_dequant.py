@@ -6,10 +6,14 @@ Each case draws a shape (1-300 rows, 1-4100 columns: odd widths, partial 64-bloc
 whole-tile multiples), an output dtype (fp16 / bf16 / fp32), a packed row stride (n/2
 or padded), the absmax sizes (the reference's full counts, or short ones that exercise
 its repeat-wrap) and the sign of the nested absmax. It runs
-``triton_dequantize_nf4`` on the GPU (flat or rows kernel, as the library picks) and
+``triton_dequantize_nf4`` on the GPU (flat or chunk kernel, as the library picks) and
 compares every output bit with the C oracle (``nf4o_dequant_ref``), which is pinned to
-the reference fallback (tests/golden/). Mismatching cases are printed with their
-parameters. One progress line per 200 cases, then a summary line.
+the reference fallback (tests/golden/). With ``--abi-rate p`` a fraction p of the cases
+calls the C ABI (``nf4_dequant_ref``) instead, with the packed weight 0-3 bytes and the
+output 0-7 elements into their allocations and a sentinel on both sides of the output
+(every load / store form of the chunk kernel, and no write outside the output).
+Mismatching cases are printed with their parameters. One progress line per 200 cases,
+then a summary line.
 """
 from __future__ import annotations
 
@@ -38,6 +42,8 @@ def draw(rng):
     kind = rng.integers(0, 4)
     if kind == 0:
         n = int(rng.integers(1, 130))                   # tiny, odd widths
+        if rng.random() < 0.3:
+            m = int(rng.integers(300, 3001))            # many rows per wave
     elif kind == 1:
         n = 64 * int(rng.integers(1, 65))               # whole 64-blocks (flat kernel)
     elif kind == 2:
@@ -57,11 +63,38 @@ def draw(rng):
     return m, n, dt, ov
 
 
+def abi_case(dev, p, a1, a2, m, n, dt, poff, ooff, want, guard=64):
+    """nf4_dequant_ref with the packed weight `poff` bytes and the output `ooff` elements
+    into their allocations; True if the output matches and the guards are untouched."""
+    from nf4_triton_dequantization_amd import _lib
+
+    tdt = {"f16": torch.float16, "bf16": torch.bfloat16, "f32": torch.float32}[dt]
+    ibits = torch.int32 if dt == "f32" else torch.int16
+    sentinel = 0x5A5A5A5A if dt == "f32" else 0x5A5A
+    big = torch.zeros(p.size + 8, dtype=torch.uint8, device=dev)
+    big[poff:poff + p.size] = torch.from_numpy(p).to(dev)
+    t1, t2 = torch.from_numpy(a1).to(dev), torch.from_numpy(a2).to(dev)
+    buf = torch.empty(guard + ooff + m * n + guard, dtype=tdt, device=dev)
+    buf.view(ibits).fill_(sentinel)
+    start = guard + ooff
+    rc = _lib.lib().nf4_dequant_ref(big.data_ptr() + poff, p.size, t1.data_ptr(), t1.numel(), t2.data_ptr(),
+                                    t2.numel(), buf.data_ptr() + start * buf.element_size(), DT[dt], m, n,
+                                    torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        return False
+    bits = buf.view(ibits).cpu().numpy()
+    if not ((bits[:start] == sentinel).all() and (bits[start + m * n:] == sentinel).all()):
+        return False
+    got = bits[start:start + m * n].view(np.uint32 if dt == "f32" else np.uint16).reshape(want.shape)
+    return bool(np.array_equal(got, want))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--seconds", type=float, default=600.0)
+    ap.add_argument("--abi-rate", type=float, default=0.0)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     orc = O.COracle()
@@ -76,8 +109,13 @@ def main():
         seed = int(rng.integers(1, 1 << 30))
         p, a1, a2, _ = O.golden_case_inputs(m, n, seed, ov)
         want = orc.dequant_ref(p, a1, a2, m, n, DT[dt])
-        got = out_bits(triton_dequantize_nf4(make_module(p, a1, a2, m, n, dt, dev)))
-        ok = np.array_equal(got.reshape(want.shape), want)
+        if rng.random() < args.abi_rate:
+            poff, ooff = int(rng.integers(0, 4)), int(rng.integers(0, 8))
+            ov = dict(ov, packed_offset=poff, out_offset=ooff)
+            ok = abi_case(dev, p, a1, a2, m, n, dt, poff, ooff, want)
+        else:
+            got = out_bits(triton_dequantize_nf4(make_module(p, a1, a2, m, n, dt, dev)))
+            ok = np.array_equal(got.reshape(want.shape), want)
         done += 1
         elements += m * n
         kinds[dt] += 1
