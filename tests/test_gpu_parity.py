@@ -265,7 +265,7 @@ def _double_rounding_scales(dt, count=64, seed=1):
 
 
 @pytest.mark.parametrize("dt", ["f16", "bf16"])
-@pytest.mark.parametrize("n", [256, 200])  # 256: flat kernel, 200: rows kernel
+@pytest.mark.parametrize("n", [256, 200])  # 256: flat kernel, 200: chunk kernel
 def test_double_rounding_and_signed_zero(coracle, gpu, dt, n):
     s, c = _double_rounding_scales(dt)
     bpr = (n + 63) // 64
