@@ -417,6 +417,12 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
     // First tile's loads go out before anything else (a wave without work
     // issues them past the buffer range: no traffic); the LUT write and the
     // barrier then overlap their latency.
+    // bitsandbytes mode: each thread's word of the 256-entry nested code goes out ahead of
+    // the tile's loads, so the wait before the barrier below covers only it (after them,
+    // the wait covered the tile's loads too: 7.48 -> 7.44 us per streamed 4096^2 launch,
+    // profiles/r05/bnb_mode_code_early.jsonl)
+    float c2w = 0.0f;
+    if constexpr (MODE == kBnb) c2w = bt.d[0].code2[threadIdx.x & 255u];
     Cursor ca = cursor_at<DT>(bt, t0, 0u);
     __amdgpu_buffer_rsrc_t rpa, roa;
     make_rsrcs<DT>(bt, ca.k, rpa, roa);
@@ -440,7 +446,11 @@ __global__ __launch_bounds__(kFlatWg) void nf4_flat_kernel(const Batch<MAXB> bt)
     if constexpr (MODE == kBnb) {  // every piece of a bitsandbytes stream carries the same code
         // (one 16-B load per lane of wave 0 ahead of everything measured slower, and no
         // table at all only 0.6 % faster: profiles/r05/bnb_mode_code_table.jsonl)
-        for (uint32_t i = threadIdx.x; i < 256u; i += kFlatWg) code2s[i] = bt.d[0].code2[i];
+        if constexpr (kFlatWg >= 256) {
+            if (threadIdx.x < 256u) code2s[threadIdx.x] = c2w;
+        } else {  // (narrower workgroups of the A/B builds)
+            for (uint32_t i = threadIdx.x; i < 256u; i += kFlatWg) code2s[i] = bt.d[0].code2[i];
+        }
     }
     __syncthreads();
     TblCtx tc{};
