@@ -592,6 +592,9 @@ constexpr uint32_t kDrop = 0xFFFFFFF0u;  // an offset past every range: load 0 /
 // of its 1 KiB span) use the default policy, so that the L2 merges a line's pieces before
 // it goes to HBM: streamed (nt) partial-line writes made odd-n matrices 16x slower.
 constexpr int kAuxPiece = 0;
+// The general form's packed loads take the default policy too: a padded row's 256-byte
+// load instructions straddle three lines, each shared with the next instruction, and nt
+// lines are not kept for it (padded 4096^2: 9.99 -> 9.61 us, profiles/r05/chunk/s45).
 // A wave's staged 16-bit span: 2048 elements + 7 of misalignment, then one dummy element
 // (past-n elements of a partial chunk), rounded to 16 bytes.
 constexpr uint32_t kStageBytes = 4128;
@@ -725,14 +728,11 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     const uint32_t r0 = fdiv(cw, A.L);
     const uint32_t q0 = cw - r0 * A.L.d;
     const uint64_t pb = (uint64_t)r0 * A.stride;
-    const uint64_t e0 = (uint64_t)r0 * A.n + 8ull * q0;  // the wave's first output element
     const __amdgpu_buffer_rsrc_t rp =
         __builtin_amdgcn_make_buffer_rsrc((void*)(A.packed + pb), 0, range32(A.packed_len - pb), kRsrcFlags);
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((char*)A.out + e0 * kOB), 0, range32((A.out_elems - e0) * kOB), kRsrcFlags);
     auto load_chunk = [&](uint32_t po) -> uint32_t {
         if constexpr (LW == 4) {
-            return __builtin_amdgcn_raw_buffer_load_b32(rp, po, 0, kAuxLoad);
+            return __builtin_amdgcn_raw_buffer_load_b32(rp, po, 0, 0);  // (see kAuxPiece)
         } else {
             uint32_t v = 0;
 #pragma unroll
@@ -745,11 +745,15 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     // per 8 chunks, and from a row's last block to the next row's first): when they number
     // at most 64, lane i gathers block g0 + i's scale once and the lanes fetch theirs with
     // ds_bpermute, as in the flat kernel; a wider span (rows of a few chunks) gathers per lane.
-    const uint32_t cl = min(cw + 255u, A.chunks - 1u);
-    const uint32_t rl = fdiv(cl, A.L);
     const uint32_t g0 = r0 * A.bpr.d + (q0 >> 3);
-    const uint32_t gl = rl * A.bpr.d + ((cl - rl * A.L.d) >> 3);
-    const bool shared = gl - g0 < 64u;
+    uint32_t gl = 0;
+    bool shared = false;
+    auto span_blocks = [&]() {  // (formed after the loads are out: nothing before them needs it)
+        const uint32_t cl = min(cw + 255u, A.chunks - 1u);
+        const uint32_t rl = fdiv(cl, A.L);
+        gl = rl * A.bpr.d + ((cl - rl * A.L.d) >> 3);
+        shared = gl - g0 < 64u;
+    };
     uint32_t w[4], rel[4], col[4], gsel[4];
     float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t ga1 = 0;
@@ -771,29 +775,29 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
         // Rows of >= 64 chunks (n >= 505): the wave touches at most 6 rows and 38 blocks
         // (shared scales), and step j+1's chunk is step j's + 64, at most one row further,
         // so every index advances by additions -- no division or multiply per step.
-        uint32_t q = q0 + lane;
-        bool wrap = q >= A.L.d;
-        q = wrap ? q - A.L.d : q;
-        uint32_t pr = wrap ? A.stride : 0u;          // (r - r0) * stride
-        uint32_t er = wrap ? A.n - 8u * q0 : 0u - 8u * q0;  // (r - r0) * n - 8 q0
-        uint32_t gr = (wrap ? A.bpr.d : 0u) + r0 * A.bpr.d - g0;  // r * bpr - g0
+        uint32_t qj[4], dr[4];  // each step's chunk within its row, and rows past r0
+        {
+            uint32_t q = q0 + lane, d = 0, pr = 0;  // pr = (r - r0) * stride
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (j) q += 64u;
+                const bool wrap = q >= A.L.d;
+                q = wrap ? q - A.L.d : q;
+                d += wrap ? 1u : 0u;
+                pr += wrap ? A.stride : 0u;
+                qj[j] = q;
+                dr[j] = d;
+                w[j] = load_chunk(cw + 64u * j + lane < A.chunks ? pr + 4u * q : kDrop);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // (the loads first; everything below waits for them anyway)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (j) {
-                q += 64u;
-                wrap = q >= A.L.d;
-                q = wrap ? q - A.L.d : q;
-                pr += wrap ? A.stride : 0u;
-                er += wrap ? A.n : 0u;
-                gr += wrap ? A.bpr.d : 0u;
-            }
             const bool ok = cw + 64u * j + lane < A.chunks;
-            w[j] = load_chunk(ok ? pr + 4u * q : kDrop);
-            col[j] = ok ? 8u * q : 0x7FFFFFF0u;  // past n (< 2^28) for every piece of a chunk past the end
-            rel[j] = er + 8u * q;
-            gsel[j] = gr + (q >> 3);
+            col[j] = ok ? 8u * qj[j] : 0x7FFFFFF0u;  // past n (< 2^28) for every piece of a chunk past the end
+            rel[j] = dr[j] * A.n + 8u * qj[j] - 8u * q0;
+            gsel[j] = dr[j] * A.bpr.d + (qj[j] >> 3) - (q0 >> 3);
         }
-        __builtin_amdgcn_sched_barrier(0);  // (keeps the scale gathers behind the loads)
     } else {
         // (indices first, then the loads, then any per-lane gathers; see opaque_mul)
         uint32_t po[4], pa1[4], pa2[4];
@@ -819,6 +823,7 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) w[j] = load_chunk(po[j]);
         __builtin_amdgcn_sched_barrier(0);
+        span_blocks();
         if (!shared) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -827,7 +832,11 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             }
         }
     }
+    if (A.L.d >= 64u) span_blocks();
     gather();  // (after the packed loads are out, as in the flat kernel)
+    const uint64_t e0 = (uint64_t)r0 * A.n + 8ull * q0;  // the wave's first output element
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((char*)A.out + e0 * kOB), 0, range32((A.out_elems - e0) * kOB), kRsrcFlags);
     float sb = 0.0f;
     if constexpr (MODE == kRef) sb = ((float)ga1 / 127.0f) * ga2;  // IEEE division (:45, :270)
     else sb = ga2;
