@@ -667,8 +667,9 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_dense_kernel(const ChunkArgs A)
     __builtin_amdgcn_sched_barrier(0);  // (the scheduler would hoist the scale gathers above them)
     // The blocks of the wave's 256 chunks are consecutive and at most 38 (rows >= 64 chunks):
     // lane i gathers block g0 + i's scale (cf. the general form below).
-    const uint32_t r0 = fdiv(cw, A.L);
-    const uint32_t q0 = cw - r0 * A.L.d;
+    const uint32_t cw0 = min(cw, A.chunks - 1u);  // (a wave wholly past the end: cf. nf4_chunk_kernel)
+    const uint32_t r0 = fdiv(cw0, A.L);
+    const uint32_t q0 = cw0 - r0 * A.L.d;
     const uint32_t cl = min(cw + 255u, A.chunks - 1u);
     const uint32_t rl = fdiv(cl, A.L);
     const uint32_t g0 = r0 * A.bpr.d + (q0 >> 3);
@@ -725,8 +726,12 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     constexpr uint32_t kOB = DT == NF4DQ_F32 ? 4u : 2u;  // output bytes per element
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t cw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
-    const uint32_t r0 = fdiv(cw, A.L);
-    const uint32_t q0 = cw - r0 * A.L.d;
+    // A wave of the last workgroup can lie wholly past the end; its row base is clamped to
+    // the last chunk's, so that the row indices every lane forms (scale gathers included)
+    // stay inside the matrix -- its loads and stores are all out of range anyway.
+    const uint32_t cw0 = min(cw, A.chunks - 1u);
+    const uint32_t r0 = fdiv(cw0, A.L);
+    const uint32_t q0 = cw0 - r0 * A.L.d;
     const uint64_t pb = (uint64_t)r0 * A.stride;
     const __amdgpu_buffer_rsrc_t rp =
         __builtin_amdgcn_make_buffer_rsrc((void*)(A.packed + pb), 0, range32(A.packed_len - pb), kRsrcFlags);
@@ -864,6 +869,7 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     };
     auto flush16 = [&]() {
         if constexpr (SW != 16) {
+            if (cw >= A.chunks) return;  // a wave wholly past the end stages nothing and writes nothing
             const uint32_t cl2 = min(cw + 255u, A.chunks - 1u);
             const uint32_t rl2 = fdiv(cl2, A.L);
             const uint32_t ql2 = cl2 - rl2 * A.L.d;

@@ -74,7 +74,7 @@ def abi_case(dev, p, a1, a2, m, n, dt, poff, ooff, want, guard=64):
     big = torch.zeros(p.size + 8, dtype=torch.uint8, device=dev)
     big[poff:poff + p.size] = torch.from_numpy(p).to(dev)
     t1, t2 = torch.from_numpy(a1).to(dev), torch.from_numpy(a2).to(dev)
-    buf = torch.empty(guard + ooff + m * n + guard, dtype=tdt, device=dev)
+    buf = torch.empty(guard + ooff + m * n + (1 << 18), dtype=tdt, device=dev)  # (wide after: stray spans)
     buf.view(ibits).fill_(sentinel)
     start = guard + ooff
     rc = _lib.lib().nf4_dequant_ref(big.data_ptr() + poff, p.size, t1.data_ptr(), t1.numel(), t2.data_ptr(),
