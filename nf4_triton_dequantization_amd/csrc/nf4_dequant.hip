@@ -567,9 +567,10 @@ __global__ __launch_bounds__(kWg) void nf4_rows_kernel(const RowsArgs A) {
 //  * nf4_chunk_kernel: the rest.  The buffer bases are the wave's first row / output
 //    element (scalar 64-bit), so only offsets within one wave's span are 32-bit; rows of
 //    >= 64 chunks advance their indices by additions, shorter rows divide per step (and
-//    gather per lane when the wave spans more than 64 blocks).  Partial chunks (n % 8 !=
-//    0) store 4- or 2-byte pieces, each past-n piece sent out of the buffer range
-//    (dropped) instead of branched around: 20.8 / 28.6 us at 4096 x 4090 / 4095.
+//    gather per lane when the wave spans more than 64 blocks).  16-bit outputs that cannot
+//    take one 16-byte store per chunk (n % 8 != 0, or the output off 16-byte alignment)
+//    are staged through LDS and written as aligned 16-byte pieces (store16 / flush16):
+//    17.9 / 15.3 us at 4096 x 4090 / 4095 (28.6 us at 4095 storing from the lanes).
 struct ChunkArgs {
     const uint8_t* packed;
     const uint8_t* a1;
@@ -588,9 +589,9 @@ struct ChunkArgs {
 };
 
 constexpr uint32_t kDrop = 0xFFFFFFF0u;  // an offset past every range: load 0 / store dropped
-// Stores of pieces narrower than 16 bytes (one wave instruction writes every 4th / 8th piece
-// of its 1 KiB span) use the default policy, so that the L2 merges a line's pieces before
-// it goes to HBM: streamed (nt) partial-line writes made odd-n matrices 16x slower.
+// Stores narrower than 16 bytes (fp32 elements of odd widths, the end pieces of a staged
+// span) use the default policy, so that the L2 merges a line's pieces before it goes to
+// HBM: streamed (nt) partial-line writes made odd-n matrices 5x slower still (s34, s35).
 constexpr int kAuxPiece = 0;
 // The general form's packed loads take the default policy too: a padded row's 256-byte
 // load instructions straddle three lines, each shared with the next instruction, and nt
@@ -716,8 +717,9 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_dense_kernel(const ChunkArgs A)
 
 // LW: 4 = dword loads (packed and stride 4-byte aligned), 1 = byte loads.
 // SW: 16 = whole-chunk 16-byte stores (16-bit output: n % 8 == 0; fp32: n % 4 == 0, two
-// per chunk; output 16-byte aligned), 4 = 4-byte pieces (16-bit: pairs, n even), 2 = single
-// 16-bit elements (odd n).
+// per chunk; output 16-byte aligned); otherwise 16-bit outputs are staged through LDS
+// (4: n even and a 4-byte aligned output, 2: the rest -- the same staged code) and fp32
+// outputs stored one element at a time.
 template <int DT, int MODE, int LW, int SW>
 __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     __shared__ __attribute__((aligned(16))) float lut[16];
