@@ -717,9 +717,8 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_dense_kernel(const ChunkArgs A)
 
 // LW: 4 = dword loads (packed and stride 4-byte aligned), 1 = byte loads.
 // SW: 16 = whole-chunk 16-byte stores (16-bit output: n % 8 == 0; fp32: n % 4 == 0, two
-// per chunk; output 16-byte aligned); otherwise 16-bit outputs are staged through LDS
-// (4: n even and a 4-byte aligned output, 2: the rest -- the same staged code) and fp32
-// outputs stored one element at a time.
+// per chunk; output 16-byte aligned); 4 = anything else: 16-bit outputs staged through
+// LDS, fp32 outputs stored one element at a time.
 template <int DT, int MODE, int LW, int SW>
 __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     __shared__ __attribute__((aligned(16))) float lut[16];
@@ -1180,14 +1179,8 @@ bool chunk_args(ChunkArgs& A, const uint8_t* packed, int64_t packed_len, void* o
 
 template <int DT, int MODE, int LW>
 void launch_chunks_lw(const ChunkArgs& A, int sw, unsigned g, hipStream_t st) {
-    if (sw == 16) {
-        hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 16>), dim3(g), dim3(kWg), 0, st, A);
-    } else if (DT == NF4DQ_F32 || sw == 4) {
-        hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 4>), dim3(g), dim3(kWg), 0, st, A);
-    } else {
-        if constexpr (DT != NF4DQ_F32)
-            hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 2>), dim3(g), dim3(kWg), 0, st, A);
-    }
+    if (sw == 16) hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 16>), dim3(g), dim3(kWg), 0, st, A);
+    else hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 4>), dim3(g), dim3(kWg), 0, st, A);
 }
 
 template <int MODE>
@@ -1202,7 +1195,7 @@ int launch_chunks(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
     const int lw = aligned(A.packed, 4) && A.stride % 4 == 0 ? 4 : 1;
     int sw;
     if (dtype == NF4DQ_F32) sw = A.n % 4 == 0 && aligned(A.out, 16) ? 16 : 4;
-    else sw = A.n % 8 == 0 && aligned(A.out, 16) ? 16 : (A.n % 2 == 0 && aligned(A.out, 4) ? 4 : 2);
+    else sw = A.n % 8 == 0 && aligned(A.out, 16) ? 16 : 4;  // (4: staged through LDS)
 #define NF4_C(DT_)                                                                 \
     do {                                                                           \
         if (lw == 4) launch_chunks_lw<DT_, MODE, 4>(A, sw, g, st);                 \
