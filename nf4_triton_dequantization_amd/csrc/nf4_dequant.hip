@@ -715,7 +715,8 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_dense_kernel(const ChunkArgs A)
     }
 }
 
-// LW: 4 = dword loads (packed and stride 4-byte aligned), 1 = byte loads.
+// LW: 4 = dword loads (packed and stride 4-byte aligned), 1 = pairs of aligned dword loads
+// joined with v_alignbyte (any alignment).
 // SW: 16 = whole-chunk 16-byte stores (16-bit output: n % 8 == 0; fp32: n % 4 == 0, two
 // per chunk; output 16-byte aligned); 4 = anything else: 16-bit outputs staged through
 // LDS, fp32 outputs stored one element at a time.
@@ -734,17 +735,24 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     const uint32_t r0 = fdiv(cw0, A.L);
     const uint32_t q0 = cw0 - r0 * A.L.d;
     const uint64_t pb = (uint64_t)r0 * A.stride;
+    // LW == 1 (a packed row start off 4-byte alignment): the buffer starts at the dword
+    // holding the wave's first byte and ends at the dword holding the weight's last, and a
+    // chunk is the two dwords around it joined with v_alignbyte_b32 -- 2 loads per chunk
+    // instead of 4 byte loads.  The at most 3 bytes read before / after the weight lie in
+    // the same dword, hence the same page, as its first / last byte.
+    const uintptr_t pw = (uintptr_t)(A.packed + pb);
+    const uint32_t kb = LW == 4 ? 0u : (uint32_t)(pw & 3u);
+    const uint64_t plen = LW == 4 ? A.packed_len - pb : ((A.packed_len - pb + kb + 3u) & ~uint64_t(3));
     const __amdgpu_buffer_rsrc_t rp =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(A.packed + pb), 0, range32(A.packed_len - pb), kRsrcFlags);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(pw - kb), 0, range32(plen), kRsrcFlags);
     auto load_chunk = [&](uint32_t po) -> uint32_t {
         if constexpr (LW == 4) {
             return __builtin_amdgcn_raw_buffer_load_b32(rp, po, 0, 0);  // (see kAuxPiece)
         } else {
-            uint32_t v = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rp, po + k, 0, 0) << (8 * k);  // (4 per line: cached)
-            return v;
+            const uint32_t a = po == kDrop ? kDrop : po + kb;  // byte offset from the aligned base
+            const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rp, a & ~3u, 0, 0);
+            const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rp, (a & ~3u) + 4u, 0, 0);
+            return __builtin_amdgcn_alignbyte(hi, lo, a & 3u);
         }
     };
     // The blocks of the wave's chunks are consecutive (block g = r * bpr + q / 8 steps by one
