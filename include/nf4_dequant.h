@@ -189,12 +189,9 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
  * only, K % 512 == 0); ksplit must equal ceil(K/128 / (waves * strips))
  * (1 = no cross-workgroup reduction). */
 #define NF4DQ_GEMM_XR 5
-/* NF4DQ_GEMM_SK: balanced ("stream-K") kernel (K % 256 == 0, M K 2 <= 64 KiB):
- * one workgroup of `waves` (8) waves per CU, the (16-column strip, 256-deep
- * chunk) units of the launch split evenly over the waves, x[M][K] in LDS;
- * strips shared by neighbouring workgroups meet in the split-K slab.  depth:
- * units in flight per wave 2/4/8 (0 = 4); strips ignored; ksplit must be 1.  Needs at least one unit per CU and at
- * most one strip (and 16 units) per wave, else NF4DQ_ERR_ARG. */
+/* NF4DQ_GEMM_SK (6): retired in round 6.  The balanced ("stream-K") kernel was
+ * never the library's choice (slower than the persistent kernel at every measured
+ * shape) and no longer ships; a cfg naming it is rejected with NF4DQ_ERR_ARG. */
 #define NF4DQ_GEMM_SK 6
 typedef struct nf4_gemm_cfg {
     int32_t kernel;

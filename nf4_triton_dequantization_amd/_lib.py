@@ -72,7 +72,7 @@ GEMM_STREAM = 2
 GEMM_PERSIST = 3
 GEMM_XS = 4
 GEMM_XR = 5
-GEMM_SK = 6
+GEMM_SK = 6  # retired in round 6: rejected with ERR_ARG
 
 
 GEMM_GROUP_MAX = 8

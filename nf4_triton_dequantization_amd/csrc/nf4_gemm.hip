@@ -147,12 +147,10 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
         const int64_t chunks = K / kChunkK, per = (int64_t)c.waves * c.strips;
         return c.ksplit == (chunks + per - 1) / per && c.ksplit <= 1024;
     }
-    if (c.kernel == NF4DQ_GEMM_SK) {
-        // static rules only: whether the launch's column total spreads over the CUs is
-        // checked at launch (sk_plan; a grouped launch counts every weight's columns)
-        return K % kSChunkK == 0 && M * K * 2 <= 65536 && c.waves == 8 && c.ksplit == 1 &&
-               (c.depth == 0 || c.depth == 2 || c.depth == 4 || c.depth == 8);
-    }
+    // NF4DQ_GEMM_SK (the balanced stream-K kernel, rounds 4-5) was never the library's
+    // choice -- 13.1-15.1 vs 10.6 us on 14336x4096 at M = 1,
+    // profiles/r04/gemm/sk_depth_vs_persist.jsonl -- and was removed in round 6: its
+    // number is rejected like any unknown kernel (git history holds the source)
     if (c.kernel == NF4DQ_GEMM_XS) {
         if (c.waves != 4 && c.waves != 8) return false;
         if (c.depth != 2 && c.depth != 4 && c.depth != 8) return false;
@@ -169,7 +167,6 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
 
 static size_t workspace_for(int64_t M, int64_t N, int64_t K, const nf4_gemm_cfg& c) {
     if (M <= 0 || N <= 0 || K <= 0 || N % 64 || K % kChunkK) return 0;
-    if (c.kernel == NF4DQ_GEMM_SK) return sk_workspace(M, K, N, c.waves);
     return c.ksplit > 1 ? counters_bytes(N) + (size_t)c.ksplit * (size_t)M * (size_t)N * 4u : 0;  // 8-B entry per 2 columns
 }
 
@@ -212,7 +209,6 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
         return launch_stream(&h, 1, x, M, K, dtype, cfg, workspace, st);
     }
     const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
-    if (cfg.kernel == NF4DQ_GEMM_SK) return launch_sk(&h, 1, x, M, K, dtype, cfg, workspace, workspace_bytes, st);
     if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(&h, 1, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_XR) return launch_xr(&h, 1, x, M, K, dtype, cfg, workspace, st);
     return launch_k128(&h, 1, x, M, K, dtype, cfg, workspace, st);
@@ -246,15 +242,14 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
         // an empty weight cannot own strip groups (the 128-deep kernel numbers
         // column groups per weight: an empty one simply owns none)
         if (mats[i].N == 0 && cfg.kernel != NF4DQ_GEMM_K128 && cfg.kernel != NF4DQ_GEMM_XS &&
-            cfg.kernel != NF4DQ_GEMM_XR && cfg.kernel != NF4DQ_GEMM_SK)
+            cfg.kernel != NF4DQ_GEMM_XR)
             return NF4DQ_ERR_SHAPE;
         if (mats[i].N == 0) continue;
         if (!valid_gemm_cfg(cfg, M, mats[i].N, K)) return NF4DQ_ERR_ARG;
         if (mats[i].packed_len >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
     }
     if (M * K * 2 >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
-    const size_t need = cfg.kernel == NF4DQ_GEMM_SK ? sk_workspace(M, K, ntot, cfg.waves)
-                        : cfg.ksplit > 1 ? kHeaderBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
+    const size_t need = cfg.ksplit > 1 ? kHeaderBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
     if (need >= (size_t(1) << 32)) return NF4DQ_ERR_TOO_LARGE;  // one buffer descriptor over the slab
     if (need && (!workspace || workspace_bytes < need || !aligned16(workspace))) return NF4DQ_ERR_ARG;
     HostMat h[NF4DQ_GEMM_GROUP_MAX];
@@ -262,7 +257,6 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
         h[i] = HostMat{mats[i].packed, mats[i].packed_len, mats[i].absmax_q, mats[i].nb, mats[i].absmax2,
                        mats[i].n2, mats[i].y, mats[i].N};
     if (cfg.kernel == NF4DQ_GEMM_K128) return launch_k128(h, count, x, M, K, dtype, cfg, workspace, st);
-    if (cfg.kernel == NF4DQ_GEMM_SK) return launch_sk(h, count, x, M, K, dtype, cfg, workspace, workspace_bytes, st);
     if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_XR) return launch_xr(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_PERSIST) {
@@ -292,8 +286,7 @@ static size_t grouped_workspace(int64_t M, int64_t K, const nf4_gemm_mat* mats, 
     if (ntot <= 0) return 0;
     nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, ntot, K);
     if (cfg.kernel == 0) cfg.kernel = default_gemm_cfg(M, ntot, K).kernel;
-    size_t w = cfg.kernel == NF4DQ_GEMM_SK ? sk_workspace(M, K, ntot, cfg.waves)
-               : cfg.ksplit > 1 ? kHeaderBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
+    size_t w = cfg.ksplit > 1 ? kHeaderBytes + (size_t)cfg.ksplit * (size_t)M * (size_t)ntot * 4u : 0;
     if (cfgp || cfg.kernel != NF4DQ_GEMM_PERSIST) return w;
     // the library's persistent choice may fall back to per-weight launches
     // (gemm_grouped_impl): the largest of their needs as well

@@ -1950,279 +1950,5 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     NF4_GSTAMP(9);
 }
 
-// ---------------------------------------------------------------------------
-// Balanced decode kernel (NF4DQ_GEMM_SK; M * K * 2 <= 64 KiB, K % 256 == 0).
-// The kernels above hand out whole 16-column strips (or groups of them) per
-// workgroup, and strips rarely divide over the CUs: 14336 columns = 896 strips
-// in groups of 4 keep 224 of 256 CUs busy (12.5 % idle), and the time until a
-// CU's first weight arrives is paid per workgroup.  Here the unit of work is one
-// (strip, 256-deep chunk) pair -- 2 KiB of packed weight, one 128-byte line of
-// each of the strip's 16 rows -- numbered strip-major over every weight of the
-// launch, and each wave of a one-workgroup-per-CU grid takes an equal
-// contiguous range of units (the "stream-K" decomposition, Osama et al.,
-// PPoPP 2023): every CU streams the same number of bytes, and a wave issues
-// its units' loads into a D-deep register ring before it builds the tables.
-//  * A wave's range is at most one strip long (host), so it holds at most two
-//    partial tiles: the end of one strip and the start of the next.
-//  * Ranges are contiguous in K within a strip, so a strip's partials are
-//    summed in range order (= K order): inside the workgroup through LDS (the x
-//    rows' region, free once every wave is done), and a strip shared with the
-//    neighbouring workgroup(s) through the split-K slab -- NOT-encoded relaxed
-//    atomics, one ticket per strip, the last arriver sums the slots in
-//    workgroup order (splitk_reduce): one launch, bitwise reproducible.  A strip
-//    shared by exactly two workgroups (the common case) meets by exchange instead
-//    (slab_swap2: one atomic round trip, the second arriver sums in slot order).
-//  * Dequant + MFMA per unit: the streaming kernels' pair-table body (sslot_mma),
-//    x[M][K] staged once per workgroup in LDS.
-//  * 8 waves per workgroup (2 per SIMD, up to 256 registers): a wave's units all
-//    in flight at once (up to 8 x 2 KiB), no register-capped drain.
-struct SkArgs {
-    StreamMat mat[kGroupMax];
-    uint32_t nmat;
-    const void* x;
-    uint64_t* slab;      // [slot][M][ncols / 2] NOT-encoded partial pairs (strips shared by > 2 workgroups)
-    uint64_t* xslab;     // [strip][M][8] exchange entries (strips shared by two workgroups)
-    uint32_t* counters;  // one ticket per strip, 0 between calls
-    uint32_t M, K;
-    FastDiv C;           // 256-deep chunks per strip (K / 256)
-    FastDiv ppr;         // 16-byte x pieces per row (K / 8)
-    uint32_t U;          // units: strips x C
-    uint32_t GW;         // waves in the grid
-    FastDiv fGW, fU;     // division by GW and by U (host: U * GW < 2^31)
-    uint32_t ncols;      // sum of N (slab row length)
-    uint32_t bpr, groups;
-    uint32_t xstride;    // LDS bytes per staged x row (16-B padded: rows 4 banks apart)
-    uint32_t zero_off;   // 128 zero bytes: the A operand of rows >= M
-};
-
-// First unit of grid wave g (g = GW: one past the last) = floor(g U / GW): the units
-// spread evenly, a wave's range differs from any other's by at most one unit.  32-bit
-// (host: U GW < 2^31), multiply-high division.
-__device__ __forceinline__ uint32_t sk_u0(const SkArgs& A, uint32_t g) { return fdiv(g * A.U, A.fGW); }
-// The grid wave whose range holds unit u: the largest g with sk_u0(g) <= u
-__device__ __forceinline__ uint32_t sk_wave_of(const SkArgs& A, uint32_t u) {
-    return fdiv((u + 1u) * A.GW - 1u, A.fU);
-}
-// The weight of a launch-wide strip (straight-line selects, uniform)
-__device__ __forceinline__ uint32_t sk_mat_of(const SkArgs& A, uint32_t strip) {
-    uint32_t mi = 0;
-#pragma unroll
-    for (int i = 1; i < kGroupMax; ++i) mi = (uint32_t)i < A.nmat && strip >= A.mat[i].strip_begin ? (uint32_t)i : mi;
-    return mi;
-}
-
-template <int DT, int W, int LM, int DMAX>
-__global__ __launch_bounds__(64 * W) void nf4_gemm_sk_kernel(const SkArgs A) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];  // x rows + zero block; later the partial tiles
-    __shared__ __attribute__((aligned(16))) f32x2 ptab[256 * 32];
-    __shared__ float qtab[256];
-    __shared__ uint32_t wrange[W][2];  // each wave's [first unit, units)
-    // ring depth: DMAX x 2 KiB per wave in flight.  All of a wave's units at once
-    // (DMAX 8: 128 KiB per CU) stalled the issue for 3.6-8.7 us at M = 1 on
-    // 14336x4096 (the address path full; the wave cannot build tables meanwhile:
-    // profiles/r04/gemm/stamps_sk_vs_persist_m1.jsonl), so the depth is a knob (cfg.depth)
-    constexpr int D = LM < DMAX ? LM : DMAX;
-    constexpr int XP = 4096 / (64 * W);  // 16-byte x pieces per thread: 64 KiB of x at most
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t nl = lane & 15u, kh = lane >> 4;
-    const uint32_t gw0 = blockIdx.x * (uint32_t)W;
-    const uint32_t u0 = sk_u0(A, gw0 + wave), n = sk_u0(A, gw0 + wave + 1u) - u0;  // n <= LM, <= C (host)
-    const uint32_t Kh = A.K >> 1;
-    NF4_GSTAMP_INIT(W);
-    NF4_GSTAMP(0);
-
-    // 1. x rows (contiguous [M][K]: piece p at byte 16 p), issued first so that the
-    //    staging below waits for them alone
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
-    const uint32_t pieces = A.M * A.ppr.d;
-    u32x4 xv[XP];
-#pragma unroll
-    for (int i = 0; i < XP; ++i) {
-        const uint32_t p = tid + (uint32_t)i * 64u * W;
-        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, p < pieces ? p * 16u : kOob, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    NF4_GSTAMP(11);
-    // 2. the ring: unit j of the wave = strip s, chunk c; lane (nl, kh) loads the 32
-    //    bytes of row nl at chunk c, quarter kh = one 64-block (one scale)
-    auto issue = [&](int j, SSlot& sl) {
-        const bool valid = (uint32_t)j < n;  // uniform; past the range: no traffic
-        const uint32_t u = valid ? u0 + (uint32_t)j : 0u;
-        const uint32_t s = fdiv(u, A.C), c = u - s * A.C.d;
-        const StreamMat& Mt = A.mat[sk_mat_of(A, s)];
-        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.packed, 0, Mt.N * Kh, kRsrcFlags);
-        const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a1, 0, Mt.nb_bytes, kRsrcFlags);
-        const __amdgpu_buffer_rsrc_t ra2 = __builtin_amdgcn_make_buffer_rsrc((void*)Mt.a2, 0, Mt.n2_bytes, kRsrcFlags);
-        const uint32_t row = (s - Mt.strip_begin) * 16u + nl;
-        const uint32_t oob = valid ? 0u : kOob;
-        const uint32_t woff = (row * Kh + c * 128u + kh * 32u) | oob;
-        sl.w0 = NF4_ABL_WLOAD(rw, woff);
-        sl.w1 = NF4_ABL_WLOAD(rw, woff + 16u);
-        // block 4c + kh of the row, nested group c (the reference's repeat wraps, :173-186)
-        sl.qa = __builtin_amdgcn_raw_buffer_load_b8(ra1, fmodu(row * A.bpr + 4u * c + kh, Mt.nb) | oob, 0, 0);
-        sl.qb = __uint_as_float(
-            __builtin_amdgcn_raw_buffer_load_b32(ra2, (fmodu(row * A.groups + c, Mt.n2) * 4u) | oob, 0, 0));
-    };
-    // the first D0 units before the tables (their data streams in while the tables are
-    // built), the rest of the ring after the barrier: a wave whose address path is full
-    // stalls at issue, and before the barrier that stall held every wave of the CU
-    constexpr int D0 = D < 2 ? D : 2;
-    SSlot ring[D];
-#pragma unroll
-    for (int j = 0; j < D0; ++j) {
-        issue(j, ring[j]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    NF4_GSTAMP(10);
-    // 3. tables (no global data: they fill while the loads fly), the x rows, one barrier
-    if (tid < 256u) qtab[tid] = (float)tid / 127.0f;  // IEEE division (:45)
-    if (tid < 8u) *reinterpret_cast<u32x4*>(smem + A.zero_off + 16u * tid) = u32x4{0u, 0u, 0u, 0u};
-    if (lane == 0) {
-        wrange[wave][0] = u0;
-        wrange[wave][1] = n;
-    }
-    for (uint32_t u = tid; u < 16u * 32u; u += 64u * W) {
-        const float clo = nf4_code(u >> 5);
-#pragma unroll
-        for (int hi = 0; hi < 16; ++hi) ptab[(16u * hi + (u >> 5)) * 32u + (u & 31u)] = f32x2{nf4_code(hi), clo};
-    }
-#pragma unroll
-    for (int i = 0; i < XP; ++i) {
-        const uint32_t p = tid + (uint32_t)i * 64u * W;
-        if (p < pieces) {
-            const uint32_t r = fdiv(p, A.ppr);
-            *reinterpret_cast<u32x4*>(smem + r * A.xstride + (p - r * A.ppr.d) * 16u) = xv[i];
-        }
-    }
-    NF4_GSTAMP(12);
-    __syncthreads();
-#pragma unroll
-    for (int j = D0; j < D; ++j) {
-        issue(j, ring[j]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    NF4_GSTAMP(1);
-
-    // 4. the wave's units in order; the partial of the first strip is set aside
-    //    when the range crosses into the next (c wraps to 0)
-    const bool live = nl < A.M;
-    const uint32_t slot8 = (lane & 31u) * 8u;
-    f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, accb[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
-    f32x4 part0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    bool split = false;
-#pragma unroll
-    for (int j = 0; j < LM; ++j) {
-        if ((uint32_t)j < n) {  // uniform
-            const uint32_t u = u0 + (uint32_t)j;
-            const uint32_t c = u - fdiv(u, A.C) * A.C.d;
-            if (j > 0 && c == 0u) {  // uniform: the range enters its second strip
-                part0 = acc[0] + accb[0];
-                acc[0] = accb[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-                split = true;
-            }
-            const uint32_t xa[1] = {live ? nl * A.xstride + c * 512u + kh * 128u : A.zero_off};
-            sslot_mma<DT, 1>(ring[j % D], ring[j % D].qa, ring[j % D].qb, ptab, qtab, smem, slot8, xa, acc, accb);
-            if (j == 0) NF4_GSTAMP(2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (j + D < LM) issue(j + D, ring[j % D]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    const f32x4 fin = acc[0] + accb[0];
-    NF4_GSTAMP(3);
-
-    // 5. partial tiles into the x region (every wave is done reading x), then per
-    //    strip of the workgroup's range one wave sums them in wave (= K) order
-    __syncthreads();
-    f32x4* red = reinterpret_cast<f32x4*>(smem);  // [W][2][64]
-    red[(wave * 2u) * 64u + lane] = split ? part0 : fin;
-    if (split) red[(wave * 2u + 1u) * 64u + lane] = fin;
-    __syncthreads();
-    NF4_GSTAMP(4);
-    const uint32_t U0 = sk_u0(A, gw0), U1 = sk_u0(A, gw0 + W);  // the workgroup's units (>= 1: host)
-    const uint32_t sA = fdiv(U0, A.C), sB = fdiv(U1 - 1u, A.C);
-    if (sA + wave <= sB) {  // uniform: this wave sums a strip
-        // every wave's range at once (one LDS round trip), in scalar registers
-        uint32_t wr0[W], wr1[W];
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            wr0[w] = __builtin_amdgcn_readfirstlane(wrange[w][0]);
-            wr1[w] = wr0[w] + __builtin_amdgcn_readfirstlane(wrange[w][1]);
-        }
-        for (uint32_t s = sA + wave; s <= sB; s += W) {  // uniform
-            const uint32_t cs = s * A.C.d, ce = cs + A.C.d;
-            // the contributing waves' partials, all reads in flight, summed in wave (= K) order
-            f32x4 v[W];
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const bool in = wr1[w] > wr0[w] && wr1[w] > cs && wr0[w] < ce;
-                v[w] = in ? red[((uint32_t)w * 2u + (wr0[w] >= cs ? 0u : 1u)) * 64u + lane]
-                          : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-            f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-            bool have = false;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const bool in = wr1[w] > wr0[w] && wr1[w] > cs && wr0[w] < ce;  // uniform
-                if (in) {
-                    sum = have ? sum + v[w] : v[w];
-                    have = true;
-                }
-            }
-            const StreamMat& Mt = A.mat[sk_mat_of(A, s)];
-            const uint32_t ycol = (s - Mt.strip_begin) * 16u;
-            if (cs >= U0 && ce <= U1) {  // the whole strip is this workgroup's: sum[r] = Y[4 kh + r][col nl]
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const uint32_t m = 4u * kh + (uint32_t)r;
-                    if (m < A.M) store_y<DT>(Mt.y, m * Mt.N + ycol + nl, sum[r]);
-                }
-                continue;
-            }
-            // shared with the neighbouring workgroup(s): slot = this workgroup's place among them
-            const uint32_t g_first = sk_wave_of(A, cs) / (uint32_t)W, g_last = sk_wave_of(A, ce - 1u) / (uint32_t)W;
-            const uint32_t slot = blockIdx.x - g_first, nsl = g_last - g_first + 1u;
-            NF4_GSTAMP(5);
-            if (nsl == 2u) {
-                // two workgroups: the hand-off by exchange (slab_swap2), one round trip;
-                // the second arriver sums in slot (= K) order, writes y, empties the entry
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const uint32_t m = 4u * kh + (uint32_t)r;
-                    const float nb = __shfl_xor(sum[r], 1, 64);
-                    if (m < A.M && !(nl & 1u)) {
-                        uint64_t* e = A.xslab + swap_entry(s, A.M, m, nl);
-                        const uint64_t g = slab_swap2(e, sum[r], nb);
-                        if (g != 0) {
-                            const float plo = __uint_as_float(~(uint32_t)g), phi = __uint_as_float(~(uint32_t)(g >> 32));
-                            const float slo = slot == 0u ? sum[r] + plo : plo + sum[r];
-                            const float shi = slot == 0u ? nb + phi : phi + nb;
-                            *reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(Mt.y) + m * Mt.N + ycol + nl) =
-                                pack2<DT>(slo, shi);
-                            __hip_atomic_store(e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                    }
-                }
-                continue;
-            }
-            const uint32_t scol = s * 16u + nl;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t m = 4u * kh + (uint32_t)r;
-                slab_put_lane(A.slab, slab_entry(slot, A.M, m, A.ncols, scol), sum[r], nl, m < A.M);
-            }
-            uint32_t last = 0;
-            if (lane == 0) last = splitk_ticket(&A.counters[s], nsl);
-            last = __builtin_amdgcn_readfirstlane(last);
-            if (last) {
-                NF4_GSTAMP(6);
-                splitk_reduce<DT, 16u>(A.slab, nsl, A.M, A.ncols, s * 16u, Mt.y, Mt.N, ycol, lane, A.counters);
-            }
-        }
-    }
-    NF4_GSTAMP(9);
-}
-
 
 }  // namespace

@@ -31,8 +31,6 @@ int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, int64_t 
               const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st);
 int launch_k128(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
                 const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st);
-int launch_sk(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
-              const nf4_gemm_cfg& cfg, void* workspace, size_t workspace_bytes, hipStream_t st);
 
 }  // namespace nf4gemm
 
@@ -134,60 +132,6 @@ inline uint32_t xr_per_wg(int64_t M, int64_t strips, const nf4_gemm_cfg& c) {
     uint32_t T = (uint32_t)((strips + P - 1) / P);
     while (T > 1 && (T > 64 || xr_lds_bytes(M, c.waves, c.strips, T) > kLdsPerCu)) T = (T + 1) / 2;
     return T < 1 ? 1u : T;
-}
-
-// Balanced kernel plan (nf4_gemm_sk_kernel): one workgroup of 8 waves per CU,
-// units = strips x (K / 256) split evenly over the waves.  Runs when x fits its
-// LDS (M K 2 <= 64 KiB), every workgroup gets a unit, and a wave's range is at
-// most one strip and 16 units long.  `slots`: most workgroups sharing one strip
-// (the split-K slab holds that many slices; 1 = no strip is shared).
-struct SkPlan {
-    uint32_t G, W, GW, C, LM, slots, xstride, zero_off, lds;
-    uint64_t U;
-};
-// static LDS of nf4_gemm_sk_kernel<., 8, .>: pair table, q/127 table, the waves' ranges;
-// the opt-in cap must keep static + dynamic within the CU's 160 KiB (an attribute
-// request beyond it fails, and its error would be the launch's hipGetLastError)
-constexpr uint32_t kSkStatic = kStreamStatic + 8u * 2u * 4u;
-constexpr uint32_t kSkLdsCap = kLdsPerCu - kSkStatic;
-
-inline bool sk_plan(int64_t M, int64_t K, int64_t ncols, int waves, SkPlan& p) {
-    if (M < 1 || M > 16 || K <= 0 || K % kSChunkK || M * K * 2 > 65536 || ncols <= 0 || ncols % 16) return false;
-    if (waves != 8) return false;
-    p.W = (uint32_t)waves;
-    p.G = (uint32_t)device_cus();
-    p.GW = p.G * p.W;
-    p.C = (uint32_t)(K / kSChunkK);
-    const uint64_t strips = (uint64_t)ncols / 16u;
-    p.U = strips * p.C;
-    if (p.U < p.G) return false;  // every workgroup gets >= 1 unit
-    const uint64_t L = (p.U + p.GW - 1) / p.GW;                 // longest wave range
-    if (L > p.C) return false;                                  // <= one strip: two partial tiles at most
-    uint32_t lm = 1;
-    while (lm < L) lm *= 2;
-    if (lm > 16) return false;
-    p.LM = lm;
-    const uint64_t GW = p.GW, U = p.U;
-    if (U * GW >= (uint64_t(1) << 31)) return false;  // the device's 32-bit range math
-    auto wg_of = [&](uint64_t u) { return ((u + 1) * GW - 1) / U / p.W; };  // sk_wave_of / W
-    uint64_t slots = 1;
-    for (uint64_t s = 0; s < strips; ++s) {
-        const uint64_t a = wg_of(s * p.C), b = wg_of(s * p.C + p.C - 1);
-        slots = b - a + 1 > slots ? b - a + 1 : slots;
-    }
-    p.slots = (uint32_t)slots;
-    p.xstride = (uint32_t)K * 2u + 16u;
-    p.zero_off = (uint32_t)M * p.xstride;
-    const uint32_t xb = p.zero_off + 128u, rb = p.W * 2u * 64u * 16u;
-    p.lds = xb > rb ? xb : rb;
-    return p.lds <= kSkLdsCap;
-}
-
-inline size_t sk_workspace(int64_t M, int64_t K, int64_t ncols, int waves) {
-    SkPlan p{};
-    if (!sk_plan(M, K, ncols, waves, p) || p.slots < 2) return 0;
-    // the ticket slab [slots][M][ncols / 2], then the exchange entries [strip][M][8]: 8 B per 2 columns each
-    return kHeaderBytes + ((size_t)p.slots + 1u) * (size_t)M * (size_t)ncols * 4u;
 }
 
 }  // namespace

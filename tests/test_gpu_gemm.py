@@ -794,69 +794,10 @@ except ImportError:  # hypothesis is part of the test environment; keep the modu
     pass
 
 
-def _sk_call(L, _lib, x, mats, dt_code, K, depth=0):
-    """One NF4DQ_GEMM_SK launch over `mats` [(packed, a1, a2, y)] through the grouped
-    ABI (one weight = a group of one); returns (rc, workspace)."""
-    import ctypes
-
-    M = x.shape[0]
-    cfg = _lib.GemmCfg(_lib.GEMM_SK, 8, depth, 1, 0)
-    arr = (_lib.GemmMat * len(mats))()
-    for i, (p, a1, a2, y) in enumerate(mats):
-        arr[i] = _lib.GemmMat(p.data_ptr(), p.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
-                              y.data_ptr(), y.shape[1])
-    wsz = L.nf4_gemm_grouped_workspace_bytes(M, K, arr, len(mats), ctypes.byref(cfg))
-    ws = torch.zeros(max(wsz, 16), dtype=torch.uint8, device=x.device)
-    st = torch.cuda.current_stream().cuda_stream
-    rc = L.nf4_gemm_ref_grouped(x.data_ptr(), M, K, arr, len(mats), dt_code, ws.data_ptr() if wsz else None, wsz,
-                                ctypes.byref(cfg), st)
-    chk = L.nf4_gemm_check_workspace(ws.data_ptr() if wsz else None, wsz, st)
-    torch.cuda.synchronize()
-    return rc, chk, ws, wsz
-
-
-@pytest.mark.parametrize("dt", ["bf16", "f16"])
-@pytest.mark.parametrize("M,Ns,K,depth", [(1, (14336,), 4096, 0), (4, (4096,), 4096, 2), (8, (1024,), 4096, 8),
-                                          (1, (4096,), 14336, 0), (3, (4160,), 1280, 4), (16, (2048,), 2048, 2),
-                                          (1, (4096, 1024, 1024), 4096, 8), (2, (14336, 14336), 4096, 2),
-                                          (5, (64, 4096, 192), 2048, 0), (1, (28672,), 4096, 8)])
-def test_balanced_kernel(coracle, gpu, dt, M, Ns, K, depth):
-    """NF4DQ_GEMM_SK: equal (strip, 256-deep chunk) ranges per wave, strips shared by
-    workgroups summed through the slab (the 1024-column weight: four workgroups per
-    strip; 4160 x 1280: ragged strip count, 5 chunks per strip; down projection: 56;
-    grouped launches with a 64-column weight inside a group; 28672 columns: 16 units per
-    wave through an 8-deep ring), every ring depth.  Checked against the
-    float64 oracle of the reference's weights, the workspace back at zero with no
-    split-K error, and a second launch bitwise identical (fixed summation order)."""
-    from nf4_triton_dequantization_amd import _lib
-
-    L = _lib.lib()
-    code = _lib.BF16 if dt == "bf16" else _lib.F16
-    xt, xb = _x_bits(M, K, dt, seed=M * 11 + K)
-    x = xt.to(gpu)
-    mats, Ws = [], []
-    for i, N in enumerate(Ns):
-        packed, a1, a2 = O.make_inputs(N, K, seed=N + K + M + 31 * i, a2_kind="normal")
-        Ws.append(coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16))
-        mats.append((torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu),
-                     torch.full((M, N), float("nan"), dtype=x.dtype, device=gpu)))
-    rc, chk, ws, wsz = _sk_call(L, _lib, x, mats, code, K, depth)
-    assert rc == 0, _lib.strerror(rc)
-    assert chk == 0, _lib.strerror(chk)
-    if wsz:
-        assert int(ws.count_nonzero()) == 0, "tickets / slab entries not back at 0"
-    first = [m[3].clone() for m in mats]
-    for (_, _, _, y), W in zip(mats, Ws):
-        assert not bool(torch.isnan(y).any())
-        _check(y, xb, W, dt)
-    rc, chk, _, _ = _sk_call(L, _lib, x, mats, code, K, depth)
-    assert rc == 0 and chk == 0
-    for y0, m in zip(first, mats):
-        assert torch.equal(y0.view(torch.int16), m[3].view(torch.int16)), "not bitwise reproducible"
-
-
-def test_balanced_kernel_rejects_what_it_cannot_spread(gpu):
-    """Fewer units than CUs, x beyond its LDS, or a K not a multiple of 256: ERR_ARG, no launch."""
+def test_retired_balanced_kernel_is_rejected(gpu):
+    """NF4DQ_GEMM_SK (the stream-K kernel, never the library's choice) was removed in
+    round 6: a cfg naming it is rejected with ERR_ARG before any device work, at shapes
+    it used to run (14336x4096 at M = 1, a grouped launch) as well as the others."""
     import ctypes
 
     from nf4_triton_dequantization_amd import _lib
@@ -864,10 +805,15 @@ def test_balanced_kernel_rejects_what_it_cannot_spread(gpu):
     L = _lib.lib()
     F = 0x1000
     c = _lib.GemmCfg(_lib.GEMM_SK, 8, 0, 1, 0)
-    for (M, N, K) in [(1, 64, 2048), (9, 4096, 4096), (1, 4096, 1152), (33, 4096, 4096)]:
+    for (M, N, K) in [(1, 14336, 4096), (4, 4096, 4096), (1, 64, 2048), (9, 4096, 4096), (1, 4096, 1152)]:
         rc = L.nf4_gemm_ref_cfg(F, M, F, N * K // 2, F, N * K // 64, F, 16, F, _lib.BF16, N, K, F, 1 << 30,
                                 ctypes.byref(c), None)
-        assert rc in (_lib.ERR_ARG, _lib.ERR_SHAPE), (M, N, K, rc)
+        assert rc == _lib.ERR_ARG, (M, N, K, rc)
+    arr = (_lib.GemmMat * 1)()
+    arr[0] = _lib.GemmMat(F, 14336 * 2048, F, 14336 * 64, F, 16, F, 14336)
+    assert L.nf4_gemm_grouped_workspace_bytes(1, 4096, arr, 1, ctypes.byref(c)) == 0
+    rc = L.nf4_gemm_ref_grouped(F, 1, 4096, arr, 1, _lib.BF16, F, 1 << 30, ctypes.byref(c), None)
+    assert rc == _lib.ERR_ARG, rc
 
 
 def _splitk3_cfg(L, _lib, x, t, y, N, K):

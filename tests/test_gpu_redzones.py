@@ -168,7 +168,6 @@ def _gemm_cfgs(K):
         for depth in (2, 4):
             for kpw in (1, 2, 4):
                 yield _lib.GemmCfg(_lib.GEMM_XR, waves, depth, -(-chunks // (waves * kpw)), kpw)
-    yield _lib.GemmCfg(_lib.GEMM_SK, 8, 0, 1, 0)  # balanced kernel (ERR_ARG where it cannot spread)
 
 
 def _gemm_ref(W_bits, x_bits):

@@ -34,6 +34,40 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 from nf4_triton_dequantization_amd import _lib  # noqa: E402
 from bench_configs import PEAK, alg_bytes, rotating_sets, rotation  # noqa: E402
 
+SHAPES = {"flat_4096": (4096, 4096, 0), "chunk_4096": (4096, 4096, _lib.CFG_CHUNKS),
+          "chunk_4080": (4096, 4080, 0), "rows_4080": (4096, 4080, _lib.CFG_ROWS),
+          "chunk_4095": (4096, 4095, 0), "chunk_4090": (4096, 4090, 0),
+          "pad_4096": (4096, 4096, 0), "unal_4096": (4096, 4096, 0)}
+# pad_4096: packed rows of 2052 bytes (n % 64 == 0 but not dense: the general form with
+# dword loads); unal_4096: the packed weight one byte into its allocation (alignbyte loads)
+PAD = {"pad_4096": 4}
+UNAL = {"unal_4096": 1}
+
+
+def case_key(name):
+    m, n, _ = SHAPES[name]
+    return (m, n, PAD.get(name, 0), UNAL.get(name, 0))
+
+
+def case_sets(name, dev, gen):
+    """(input sets, output sets) of a case, rotated as bench.py rotates (>= 512 MiB of
+    distinct reads and of writes: HBM-streamed)."""
+    m, n, _ = SHAPES[name]
+    key = case_key(name)
+    pin, pout = rotation(m, n, 2)
+    if n % 2 or key[2] or key[3]:  # packed rows of ceil(n/2) + pad bytes, at byte offset unal
+        ins = []
+        stride = (n + 1) // 2 + key[2]
+        for _ in range(pin):
+            nb = m * n // 64 + 1
+            q = torch.randint(0, 256, (m * stride + key[3],), dtype=torch.uint8, device=dev, generator=gen)
+            ins.append((q[key[3]:],
+                        torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen),
+                        torch.rand((nb + 255) // 256, device=dev, generator=gen) * 0.01 + 1e-3))
+        outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(pout)]
+        return ins, outs
+    return rotating_sets(m, n, torch.bfloat16, dev, gen, pin, pout)
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -58,42 +92,20 @@ def main():
     e1.record(st)
     torch.cuda.synchronize()
     cyc_per_us = 2_000_000 / max(e0.elapsed_time(e1) * 1e3, 1.0)
-    shapes = {"flat_4096": (4096, 4096, 0), "chunk_4096": (4096, 4096, _lib.CFG_CHUNKS),
-              "chunk_4080": (4096, 4080, 0), "rows_4080": (4096, 4080, _lib.CFG_ROWS),
-              "chunk_4095": (4096, 4095, 0), "chunk_4090": (4096, 4090, 0),
-              "pad_4096": (4096, 4096, 0), "unal_4096": (4096, 4096, 0)}
-    # pad_4096: packed rows of 2052 bytes (n % 64 == 0 but not dense: the general form with
-    # dword loads); unal_4096: the packed weight one byte into its allocation (byte loads)
-    pad = {"pad_4096": 4}
-    unal = {"unal_4096": 1}
     gen = torch.Generator(device=dev)
     gen.manual_seed(3)
     sets = {}
     for name in args.cases.split(","):
-        m, n, flags = shapes[name]
-        key = (m, n, pad.get(name, 0), unal.get(name, 0))
+        key = case_key(name)
         if key not in sets:
-            pin, pout = rotation(m, n, 2)
-            if n % 2 or key[2] or key[3]:  # packed rows of ceil(n/2) + pad bytes, at byte offset unal
-                ins = []
-                stride = (n + 1) // 2 + key[2]
-                for _ in range(pin):
-                    nb = m * n // 64 + 1
-                    q = torch.randint(0, 256, (m * stride + key[3],), dtype=torch.uint8, device=dev, generator=gen)
-                    ins.append((q[key[3]:],
-                                torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen),
-                                torch.rand((nb + 255) // 256, device=dev, generator=gen) * 0.01 + 1e-3))
-                outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(pout)]
-            else:
-                ins, outs = rotating_sets(m, n, torch.bfloat16, dev, gen, pin, pout)
-            sets[key] = (ins, outs)
+            sets[key] = case_sets(name, dev, gen)
     cfgs = {f: _lib.LaunchCfg(4, 0, 1, f) for f in (_lib.CFG_CHUNKS, _lib.CFG_ROWS)}
 
     def launcher(tag):
         lname, name = tag.split(":")
         L = libs[lname]
-        m, n, flags = shapes[name]
-        ins, outs = sets[(m, n, pad.get(name, 0), unal.get(name, 0))]
+        m, n, flags = SHAPES[name]
+        ins, outs = sets[(m, n, PAD.get(name, 0), UNAL.get(name, 0))]
 
         def launch(i):
             q, a1, a2 = ins[i % len(ins)]
@@ -112,7 +124,7 @@ def main():
     fns = {nm: launcher(nm) for nm in names}
     for nm in names:  # every set touched once
         c = nm.split(":")[1]
-        ins, outs = sets[shapes[c][:2] + (pad.get(c, 0), unal.get(c, 0))]
+        ins, outs = sets[SHAPES[c][:2] + (PAD.get(c, 0), UNAL.get(c, 0))]
         for i in range(max(len(ins), len(outs))):
             fns[nm](i)
     torch.cuda.synchronize()
@@ -129,7 +141,7 @@ def main():
             torch.cuda.synchronize()
             res[nm].append(e0.elapsed_time(e1) * 1e3 / args.steps)
     for nm in names:
-        m, n, flags = shapes[nm.split(":")[1]]
+        m, n, flags = SHAPES[nm.split(":")[1]]
         ts = sorted(res[nm])
         med = ts[len(ts) // 2]
         byt = alg_bytes(m, n, 2)

@@ -59,11 +59,12 @@ __device__ __forceinline__ unsigned long long nf4_gs_now() {
         __builtin_amdgcn_sched_barrier(0);                                                                \
     } while (0)
 
+// ablation hooks (none unless -DABL_<part>: the gstamps_<part> builds)
+#include "gemm_ablate_hooks.h"
 // the product's fused-GEMM sources, all in this one translation unit
 #include "../nf4_triton_dequantization_amd/csrc/nf4_gemm.hip"
 #include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_k128.hip"
 #include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_persist.hip"
-#include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_sk.hip"
 #include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_stream.hip"
 #include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_xr.hip"
 #include "../nf4_triton_dequantization_amd/csrc/nf4_gemm_launch_xs.hip"

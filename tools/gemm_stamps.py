@@ -26,7 +26,11 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-os.environ["NF4DQ_LIB_PATH"] = os.path.join(REPO, "tools", "_build", "libnf4dq_gstamps.so")
+# --variant <part>: a stamped ablation build (tools/Makefile libnf4dq_gstamps_<part>.so,
+# e.g. skeleton); parsed before the library is imported, since the import loads it
+_VAR = next((sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a == "--variant"), "")
+os.environ["NF4DQ_LIB_PATH"] = os.path.join(REPO, "tools", "_build",
+                                            f"libnf4dq_gstamps_{_VAR}.so" if _VAR else "libnf4dq_gstamps.so")
 from nf4_triton_dequantization_amd import _lib  # noqa: E402
 
 
@@ -44,6 +48,7 @@ def main():
     ap.add_argument("--m", type=int, default=32)
     ap.add_argument("--cfg", action="append", default=[], help="kernel,waves,depth,ksplit,strips (default: library)")
     ap.add_argument("--launches", type=int, default=8)
+    ap.add_argument("--variant", default="", help="stamped ablation build (e.g. skeleton); default: the product")
     args = ap.parse_args()
     L = _lib.lib()
     L.nf4_dbg_set_gemm_stamps.argtypes = [ctypes.c_void_p]
@@ -111,7 +116,7 @@ def main():
             rows["handoff"].append(s9 - s5)
             rows["end"].append(s9 - t0)
             spans.append(np.nanmax(s9) - t0)
-        out = {"cfg": cs or "library", "N": n, "K": k, "M": M, "waves_per_launch": int(len(rows["start"][0])),
+        out = {"variant": args.variant or "product", "cfg": cs or "library", "N": n, "K": k, "M": M, "waves_per_launch": int(len(rows["start"][0])),
                "span_us": pct(spans)}
         for key, v in rows.items():
             out[key] = pct(np.concatenate(v))

@@ -80,6 +80,42 @@ def main():
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / 1e3
         total += t
+        # the same loop's pieces: host time to issue it, the three
+        # torch.cuda.Stream() creations alone, and the three drop-in calls alone on the
+        # current stream (no new streams), each per iteration
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        for _ in range(args.iterations):
+            mlp_dequantize(mlp, triton_dequantize_nf4, sync=False)
+        host_loop_us = (time.perf_counter() - h0) * 1e6 / args.iterations
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        for _ in range(args.iterations):
+            _s = (torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream())
+        streams_us = (time.perf_counter() - h0) * 1e6 / args.iterations
+        del _s
+        mods3 = [mlp.up_proj, mlp.gate_proj, mlp.down_proj]
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        for _ in range(args.iterations):
+            for md in mods3:
+                triton_dequantize_nf4(md).t()
+        calls_us = (time.perf_counter() - h0) * 1e6 / args.iterations
+        torch.cuda.synchronize()
+        # device time of the three single launches (one stream, graph replay)
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            outs1 = [triton_dequantize_nf4(md) for md in mods3]
+        g1.replay()
+        torch.cuda.synchronize()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record()
+        for _ in range(50):
+            g1.replay()
+        r1.record()
+        torch.cuda.synchronize()
+        dev1_us = r0.elapsed_time(r1) * 1e3 / 50
+        del outs1, g1
         # device-only time of the same three dequantizations (graph replay, batched launch)
         mods = [mlp.up_proj, mlp.gate_proj, mlp.down_proj]
         g = torch.cuda.CUDAGraph()
@@ -98,6 +134,10 @@ def main():
         print(json.dumps({"config": f"hd={hd} m={m} {str(dt).replace('torch.', '')}",
                           "iterations": args.iterations, "seconds": t, "us_per_iteration": t * 1e6 / args.iterations,
                           "device_us_per_iteration_batched_graph": dev_us,
+                          "device_us_per_iteration_three_launches_graph": dev1_us,
+                          "host_us_per_iteration_issue": host_loop_us,
+                          "host_us_three_stream_creations": streams_us,
+                          "host_us_three_dropin_calls_current_stream": calls_us,
                           "elements_per_iteration": elems}), flush=True)
         del outs, g
     # host cost of one API call (device work hidden behind a long queue)

@@ -51,19 +51,31 @@ def main():
     cw, _ = mean_for(write, "calib_write_x4")
     rf = CALIB_BYTES / (cr * 1024.0)
     wf = CALIB_BYTES / (cw * 1024.0)
-    kf, nf = mean_for(fetch, "nf4_flat_kernel")
-    kw, nw = mean_for(write, "nf4_flat_kernel")
+    # PMC_KERNEL: the kernel name to average (default the flat kernel; nf4_chunk for
+    # tools/pmc_chunk.py's forms, whose shape PMC_CASE names)
+    kname = os.environ.get("PMC_KERNEL", "nf4_flat_kernel")
+    case = os.environ.get("PMC_CASE")
+    if case:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from chunk_ab import SHAPES
+        m, n, _ = SHAPES[case]
+    kf, nf = mean_for(fetch, kname)
+    kw, nw = mean_for(write, kname)
     fetch_b = kf * 1024.0 * rf
     write_b = kw * 1024.0 * wf
     N = m * n
     alg_r = N // 2 + N // 64 + 4 * ((N // 64 + 255) // 256)
     alg_w = 2 * N
-    res = {"m": m, "n": n, "dtype": os.environ.get("PMC_DTYPE", "bf16"),
+    if case:  # tools/chunk_ab.py's algorithmic bytes (its frac): SURVEY 8(d) per element
+        from bench_configs import alg_bytes
+        alg_r = alg_bytes(m, n, 2) - 2 * N
+    res = {"m": m, "n": n, "dtype": os.environ.get("PMC_DTYPE", "bf16"), "kernel": kname, "case": case,
            "fetch_kib_raw": kf, "write_kib_raw": kw, "dispatches": [nf, nw],
            "read_factor_dword_loads": rf, "write_factor_x4_nt_stores": wf,
            "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
            "hbm_bytes_per_launch": fetch_b + write_b,
            "algorithmic_read_bytes": alg_r, "algorithmic_write_bytes": alg_w,
+           "read_over_algorithmic": fetch_b / alg_r, "write_over_algorithmic": write_b / alg_w,
            "traffic_over_algorithmic": (fetch_b + write_b) / (alg_r + alg_w)}
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:

@@ -41,7 +41,6 @@ CASES = [  # (label, M, N, K, cfg or None for the library default)
     ("stream ksplit 4", 8, 4096, 4096, G.GemmCfg(G.GEMM_STREAM, 8, 2, 4, 4)),
     ("k128 ksplit 4", 32, 2048, 4096, G.GemmCfg(G.GEMM_K128, 8, 1, 4, 4)),
     ("xs (shared activation) ksplit 4", 32, 6144, 4096, G.GemmCfg(G.GEMM_XS, 4, 8, 4, 1)),
-    ("balanced (stream-K)", 1, 14336, 4096, G.GemmCfg(G.GEMM_SK, 8, 0, 1, 0)),
     ("library default M = 32", 32, 14336, 4096, None),
     ("library default M = 16", 16, 14336, 4096, None),
 ]
