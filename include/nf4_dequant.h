@@ -51,7 +51,17 @@ extern "C" {
  *   absmax_q uint8[nb]          per (row, 64-column block); index wraps mod nb
  *   absmax2  fp32[n2]           index r*ceil(bpr/4) + block/4, wraps mod n2
  * out[r][c] = RNE(NF4[nib] * ((float)absmax_q[.] / 127.0f * absmax2[.])).
- * Errors: packed_len % m != 0 or packed_len/m < ceil(n/2) -> NF4DQ_ERR_SHAPE. */
+ * Errors: packed_len % m != 0 or packed_len/m < ceil(n/2) -> NF4DQ_ERR_SHAPE.
+ *
+ * Departure from SURVEY.md §8(b): the survey's contract is
+ *   nf4_dequant_ref(packed, absmax_q, nb, absmax2, n2, out, out_dtype, m, n, hip_stream);
+ * this entry (and nf4_dequant_ref_cpu, nf4_dequant_single, nf4_dequant_single_cpu)
+ * adds `packed_len` right after `packed`.  The reference reads the packed weight as
+ * `weight.data.view(m, -1)` (kernel_optimized.py:229), so the row stride is
+ * numel / m -- padded rows and odd widths included (:288-312) -- and a pointer
+ * alone does not carry numel.  Without it the ABI could only assume the dense
+ * stride ceil(n/2) and would silently misread padded weights the reference
+ * accepts; with it, sizes the reference's view would reject are NF4DQ_ERR_SHAPE. */
 int nf4_dequant_ref(const uint8_t* packed, int64_t packed_len,
                     const uint8_t* absmax_q, int64_t nb,
                     const float* absmax2, int64_t n2,

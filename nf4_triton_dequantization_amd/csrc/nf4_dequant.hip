@@ -869,10 +869,24 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             const u32x4 o = {p[0], p[1], p[2], p[3]};
             __builtin_amdgcn_raw_buffer_store_b128(o, ro, col[j] < A.n ? rel[j] * 2u : kDrop, 0, kAuxStore);
         } else {
+            // All 8 elements go to the stage at 2 (rel + sa) + 2 i, past-n ones included (round 6:
+            // one address per chunk instead of a compare + select per element).  A row's last,
+            // partial chunk thus writes its past-n elements onto the first slots of the chunks
+            // that follow it in the span; the rightful element of such a slot always has a
+            // SMALLER index i in its own chunk than the past-n element that lands on it, and every
+            // lane writes its elements from i = 7 down to 0, so the rightful one is written last
+            // (the chunk after lane 63's is lane 0's at step j + 1: later in program order too).
+            // The slack past the span's end covers the last chunk's past-n elements; chunks past
+            // the end of the matrix write to the dummy slots.
+            const bool ok = cw + 64u * (uint32_t)j + lane < A.chunks;
+            char* a = stage + sbase + (ok ? 2u * (rel[j] + sa) : kStageDummy);
+            // (the compiler barrier keeps the 8 stores apart: merged into one unaligned
+            // ds_write_b128, a past-n element and the slot's rightful one would be written by
+            // two lanes of the same instruction, in no defined order)
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t off = col[j] + i < A.n ? 2u * (rel[j] + i + sa) : kStageDummy;
-                *reinterpret_cast<u16_alias*>(stage + sbase + off) = (uint16_t)(p[i >> 1] >> (16 * (i & 1)));
+            for (int i = 7; i >= 0; --i) {
+                reinterpret_cast<u16_alias*>(a)[i] = (uint16_t)(p[i >> 1] >> (16 * (i & 1)));
+                asm volatile("" ::: "memory");
             }
         }
     };
@@ -883,6 +897,11 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             const uint32_t rl2 = fdiv(cl2, A.L);
             const uint32_t ql2 = cl2 - rl2 * A.L.d;
             const uint32_t span = (uint32_t)((uint64_t)rl2 * A.n + min(8u * ql2 + 8u, A.n) - e0);
+            // the span's own range: an end piece's elements outside it (another wave's) are
+            // dropped by the descriptor's range check -- below its start their offsets wrap
+            // past 2^31 -- so they need no compare each
+            const __amdgpu_buffer_rsrc_t rsp =
+                __builtin_amdgcn_make_buffer_rsrc((void*)((char*)A.out + e0 * 2u), 0, 2u * span, kRsrcFlags);
 #pragma unroll
             for (int st = 0; st < 5; ++st) {
                 const int x0 = (int)(8u * (lane + 64u * st)) - (int)sa;  // piece k = lane + 64 st
@@ -892,12 +911,9 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
                 __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxStore);
                 if (!whole) {
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const int x = x0 + i;
-                        const uint16_t e = (uint16_t)(v[i >> 1] >> (16 * (i & 1)));
-                        __builtin_amdgcn_raw_buffer_store_b16(e, ro, x >= 0 && x < (int)span ? 2u * (uint32_t)x : kDrop, 0,
-                                                              kAuxPiece);
-                    }
+                    for (int i = 0; i < 8; ++i)
+                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[i >> 1] >> (16 * (i & 1))), rsp,
+                                                              2u * (uint32_t)(x0 + i), 0, kAuxPiece);
                 }
             }
         }

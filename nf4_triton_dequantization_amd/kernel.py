@@ -429,12 +429,15 @@ def _gemm_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
 
 
 def release_gemm_workspaces() -> None:
-    """Forget every cached split-K workspace (after a synchronize of their streams):
-    for callers that destroy their own external streams."""
-    for (dev_index, _), (ws, stream) in list(_GEMM_WS.items()):
-        with torch.cuda.device(dev_index):
-            stream.synchronize()
-    _GEMM_WS.clear()
+    """Forget every cached split-K workspace: for callers that destroy their own external
+    streams.  Each workspace's sticky error word is read first (which also waits for its
+    stream), so a split-K timeout since the last ``check_gemm_workspaces()`` is not lost
+    with the workspace: the cache is cleared either way, then RuntimeError is raised as
+    ``check_gemm_workspaces`` would."""
+    try:
+        check_gemm_workspaces()
+    finally:
+        _GEMM_WS.clear()
 
 
 def check_gemm_workspaces() -> None:

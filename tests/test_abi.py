@@ -28,6 +28,59 @@ def test_library_exports_every_declared_symbol():
         assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
 
 
+_CTYPE_OF = {  # C parameter / return type in the header -> the ctypes type the binding must use
+    "int": ctypes.c_int, "int32_t": ctypes.c_int32, "int64_t": ctypes.c_int64, "size_t": ctypes.c_size_t,
+    "float": ctypes.c_float, "void*": ctypes.c_void_p, "const void*": ctypes.c_void_p,
+    "const uint8_t*": ctypes.c_void_p, "const float*": ctypes.c_void_p, "const char*": ctypes.c_char_p,
+    "const nf4_matrix_desc*": ctypes.POINTER(_lib.MatrixDesc), "const nf4_launch_cfg*": ctypes.POINTER(_lib.LaunchCfg),
+    "const nf4_gemm_cfg*": ctypes.POINTER(_lib.GemmCfg), "const nf4_gemm_mat*": ctypes.POINTER(_lib.GemmMat),
+}
+
+
+def _header_prototypes():
+    """name -> (return C type, [parameter C types]) for every prototype of the header."""
+    text = re.sub(r"/\*.*?\*/", "", open(_lib.HEADER_PATH).read(), flags=re.S)
+    protos = {}
+    for ret, name, params in re.findall(r"^\s*((?:const\s+)?\w+\s*\*?)\s*(nf4_\w+)\s*\(([^)]*)\)\s*;", text,
+                                        flags=re.M):
+        types = []
+        for p in [p.strip() for p in params.split(",") if p.strip() and p.strip() != "void"]:
+            p = re.sub(r"\s*\*\s*", "* ", p)           # "T *x" / "T* x" -> "T* x"
+            types.append(p.rsplit(" ", 1)[0].strip())  # drop the parameter name
+        protos[name] = (re.sub(r"\s*\*", "*", ret.strip()), types)
+    return protos
+
+
+def test_binding_argtypes_equal_header_prototypes():
+    """Every exported entry's ctypes restype/argtypes are exactly the header's C types,
+    parameter by parameter (a drifted binding would pass wrong-width integers)."""
+    protos = _header_prototypes()
+    assert sorted(protos) == _header_functions()
+    for name, (ret, params) in protos.items():
+        res, args = _lib.SIGNATURES[name]
+        assert res == _CTYPE_OF[ret], (name, ret, res)
+        assert len(args) == len(params), (name, params, args)
+        for i, (c, t) in enumerate(zip(params, args)):
+            assert t == _CTYPE_OF[c], (name, i, c, t)
+        fn = getattr(_lib.lib(), name)
+        assert fn.restype == res and list(fn.argtypes) == list(args), name
+
+
+def test_survey_8b_signature_departure_is_packed_len_only():
+    """SURVEY §8(b) specifies nf4_dequant_ref(packed, absmax_q, nb, absmax2, n2, out,
+    out_dtype, m, n, hip_stream).  The header adds exactly one parameter, `packed_len`
+    after `packed` (the reference's `.view(m, -1)` row stride, kernel_optimized.py:229),
+    and the departure is recorded in the header itself."""
+    survey = ["const uint8_t*", "const uint8_t*", "int64_t", "const float*", "int64_t", "void*", "int32_t",
+              "int64_t", "int64_t", "void*"]
+    _, params = _header_prototypes()["nf4_dequant_ref"]
+    assert params[:1] + params[2:] == survey and params[1] == "int64_t"
+    _, cpu = _header_prototypes()["nf4_dequant_ref_cpu"]
+    assert cpu[:-1] == params[:-1] and cpu[-1] == "int32_t"  # host form: `threads` for the stream
+    text = open(_lib.HEADER_PATH).read()
+    assert "Departure from SURVEY.md §8(b)" in text and "packed_len" in text
+
+
 def test_header_constants_match_binding():
     text = open(_lib.HEADER_PATH).read()
     consts = dict(re.findall(r"#define\s+(NF4DQ_\w+)\s+(\d+)", text))

@@ -97,6 +97,16 @@ def test_world_size_must_match_gpus():
     assert p.returncode != 0 and "must agree" in p.stderr
 
 
+@pytest.mark.timeout(120)
+def test_nccl_needs_a_gpu_per_rank():
+    """--dist-backend nccl with more ranks than visible GPUs (here: none) stops before
+    set_device / the RCCL rendezvous, non-zero, with a plain message."""
+    p = _run(["--gpus", "2", "--dist-backend", "nccl", "--steps", "1", "--no-cpu-baseline"],
+             env_extra={"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"}, timeout=110)
+    assert p.returncode != 0
+    assert "needs one GPU per rank" in p.stderr and "WORLD_SIZE=2" in p.stderr, p.stderr[-2000:]
+
+
 def test_c5_partition_covers_every_matrix_once():
     sys.path.insert(0, REPO)
     import bench

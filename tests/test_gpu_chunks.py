@@ -1,13 +1,21 @@
-"""The chunk kernel (``-m gpu``): every shape the flat kernel does not take.
+"""The chunk kernels (``-m gpu``): every shape the flat kernel does not take.
 
-n % 64 != 0, padded packed rows and unaligned pointers go through nf4_chunk_kernel
-(csrc/nf4_dequant.hip).  Its load form (dword / byte) and store form (16-byte chunks,
-4-byte pieces, 2-byte elements) are picked from n, the row stride and the pointer
-alignment; these cases run every combination through the C ABI in both scale modes
-and compare bit for bit with the C oracle, and check that no byte outside the output
-is written (past-n pieces are dropped by the buffer range, not branched around).
-The NF4DQ_CFG_CHUNKS / NF4DQ_CFG_ROWS tuning flags cross-check the chunk kernel
-against the flat kernel and the one-thread-per-byte kernel.
+n % 64 != 0, padded packed rows and unaligned pointers go through the chunk kernels of
+csrc/nf4_dequant.hip.  Which instantiation a shape takes (launch_chunks):
+* nf4_chunk_dense_kernel -- 16-bit output, n % 8 == 0, packed rows of exactly 4 L bytes
+  (L = chunks per row >= 64), 4-byte-aligned packed weight, 16-byte-aligned output;
+* nf4_chunk_kernel<LW, SW> otherwise, with the load form LW = 4 (dword loads: packed
+  weight and row stride 4-byte aligned) or 1 (two aligned dwords per chunk joined with
+  v_alignbyte: any alignment), and the store form SW = 16 (one 16-byte store per chunk,
+  or two for fp32: n % 8 == 0 (fp32: n % 4 == 0) and a 16-byte-aligned output) or 4
+  (16-bit outputs staged through LDS and written as aligned 16-byte pieces, the span's
+  two end pieces element by element; fp32 stored one element at a time); rows of >= 64
+  chunks advance their indices by additions, shorter ones divide per step.
+These cases run every form through the C ABI in both scale modes and compare bit for bit
+with the C oracle, with sentinels on both sides of the output (past-n pieces are dropped
+by the buffer range, not branched around).  The NF4DQ_CFG_CHUNKS / NF4DQ_CFG_ROWS tuning
+flags cross-check the chunk kernels against the flat kernel and the one-thread-per-byte
+kernel.  Waves wholly past the end of a matrix: tests/test_gpu_edges.py.
 """
 import ctypes
 
@@ -78,24 +86,25 @@ def _ref_call(dev, p, a1, a2, m, n, dt, p_off=0, o_elem_off=0, flags=None):
     return buf, start
 
 
-# (m, n, extra stride bytes, packed byte offset, output element offset): the forms they select
+# (m, n, extra stride bytes, packed byte offset, output element offset): the form each
+# selects for 16-bit output (fp32: the general form, SW 16 when n % 4 == 0 and aligned)
 CASES = [
-    (37, 1000, 0, 0, 0),      # n % 8 == 0, dense rows >= 64 chunks: the dense form
-    (5, 4080, 0, 0, 0),
-    (33, 1000, 4, 0, 0),      # padded rows of >= 64 chunks: dword loads, 16-byte chunk stores
-    (9, 4080, 0, 0, 1),       # output off 16-byte alignment: 4-byte pieces
-    (9, 1002, 0, 0, 0),       # n % 8 == 2: 4-byte pieces (16-bit) / 4-byte elements (fp32)
-    (3, 6, 0, 0, 0),
-    (7, 77, 0, 0, 0),         # odd n: 2-byte elements, byte loads (stride 39)
+    (37, 1000, 0, 0, 0),      # n % 8 == 0, rows of exactly 4 L bytes, L >= 64: the dense form
+    (5, 4080, 0, 0, 0),       # (the dense form)
+    (33, 1000, 4, 0, 0),      # padded rows: LW 4 (dword loads), SW 16 (16-byte chunk stores)
+    (9, 4080, 0, 0, 1),       # output off 16-byte alignment: LW 4, SW 4 (staged)
+    (9, 1002, 0, 0, 0),       # n % 8 == 2, stride 501: LW 1 (alignbyte pairs), SW 4 (staged)
+    (3, 6, 0, 0, 0),          # L = 1: LW 1, SW 4, per-step row division
+    (7, 77, 0, 0, 0),         # odd n (stride 39): LW 1, SW 4
     (1, 1, 0, 0, 0),
     (4, 3, 0, 0, 0),
-    (11, 200, 3, 0, 0),       # padded rows, stride % 4 != 0: byte loads
-    (11, 200, 4, 0, 0),       # padded rows, stride % 4 == 0: dword loads
-    (6, 256, 2, 0, 0),        # n % 64 == 0 but padded: not flat
-    (6, 256, 0, 1, 0),        # odd packed pointer
-    (6, 256, 0, 2, 1),        # output one element off 16-byte alignment
-    (10, 1000, 0, 3, 3),
-    (3000, 2, 0, 0, 0),       # one chunk per row: 256 rows per wave
+    (11, 200, 3, 0, 0),       # padded rows, stride % 4 != 0: LW 1, SW 16, L < 64
+    (11, 200, 4, 0, 0),       # padded rows, stride % 4 == 0: LW 4, SW 16, L < 64
+    (6, 256, 2, 0, 0),        # n % 64 == 0 but padded: not flat (LW 1)
+    (6, 256, 0, 1, 0),        # odd packed pointer: LW 1
+    (6, 256, 0, 2, 1),        # output one element off 16-byte alignment: SW 4
+    (10, 1000, 0, 3, 3),      # LW 1, SW 4, L >= 64
+    (3000, 2, 0, 0, 0),       # one chunk per row: 256 rows per wave (per-lane scale gathers)
     (300, 18, 5, 0, 1),
     (129, 4100, 0, 0, 0),     # partial last wave
 ]
@@ -117,9 +126,10 @@ def test_chunk_kernel_forms_vs_oracle(coracle, gpu, dt, m, n, pad, poff, ooff):
 def test_single_quant_chunk_kernel(coracle, gpu, dt):
     L = _lib().lib()
     # (48 x 269 and 51 x 275: the last workgroup has a wave wholly past the end, whose row
-    # index once ran past the absmax rows -- an out-of-range gather, seen by fuzz_api seed 61)
+    # index once ran past the absmax rows -- an out-of-range gather, seen by fuzz_api seed 61;
+    # 37 x 1000 and 5 x 4080 unpadded: the dense form's kSingle scale gather)
     for (m, n, extra, pad) in ((12, 200, 0, 0), (6, 1002, 3, 1), (33, 77, 1, 0), (5, 4080, 2, 4), (48, 269, 0, 0),
-                               (51, 275, 2, 0), (122, 261, 1, 0)):
+                               (51, 275, 2, 0), (122, 261, 1, 0), (37, 1000, 0, 0), (5, 4080, 1, 0)):
         stride = (n + 1) // 2 + pad
         p, _, _, single = O.golden_case_inputs(m, n, m + n, {"single": extra, "stride": stride})
         want = coracle.dequant_single(p, single, m, n, DT_CODE[dt])

@@ -49,13 +49,17 @@ def main():
     ap.add_argument("--cfg", action="append", default=[], help="kernel,waves,depth,ksplit,strips (default: library)")
     ap.add_argument("--launches", type=int, default=8)
     ap.add_argument("--variant", default="", help="stamped ablation build (e.g. skeleton); default: the product")
+    ap.add_argument("--chain", type=int, default=1,
+                    help="launches back to back per sample (other copies first, no sync between): the stamps "
+                         "are the last launch's, in the regime of a decode pass / bench (default 1: alone, cold)")
     args = ap.parse_args()
     L = _lib.lib()
     L.nf4_dbg_set_gemm_stamps.argtypes = [ctypes.c_void_p]
     dev = torch.device("cuda", 0)
     n, k = (int(v) for v in args.shape.split(","))
     M = args.m
-    copies = max(4, (512 << 20) // (n * k // 2))
+    # distinct copies: a chain's weights stream from HBM, not the 256 MiB Infinity Cache
+    copies = max(4, 2 * args.chain, (1024 << 20) // (n * k // 2))
     nb = n * k // 64
     ws = [(torch.randint(0, 256, (n * k // 2,), dtype=torch.uint8, device=dev),
            torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev),
@@ -75,9 +79,20 @@ def main():
                                     "end")}
         spans = []
         for it in range(args.launches + 2):
-            q, a1, a2 = ws[it % copies]
+            q, a1, a2 = ws[(it * args.chain) % copies]
             stamps.zero_()
             torch.cuda.synchronize()
+            for c in range(args.chain - 1):  # earlier launches of the chain: their stamps are overwritten
+                qc, a1c, a2c = ws[(it * args.chain + c + 1) % copies]
+                if cfg is not None:
+                    rc = L.nf4_gemm_ref_cfg(x.data_ptr(), M, qc.data_ptr(), qc.numel(), a1c.data_ptr(), a1c.numel(),
+                                            a2c.data_ptr(), a2c.numel(), y.data_ptr(), _lib.BF16, n, k,
+                                            work.data_ptr(), work.numel(), ctypes.byref(cfg), sp)
+                else:
+                    rc = L.nf4_gemm_ref(x.data_ptr(), M, qc.data_ptr(), qc.numel(), a1c.data_ptr(), a1c.numel(),
+                                        a2c.data_ptr(), a2c.numel(), y.data_ptr(), _lib.BF16, n, k,
+                                        work.data_ptr(), work.numel(), sp)
+                assert rc == 0, rc
             if cfg is not None:
                 rc = L.nf4_gemm_ref_cfg(x.data_ptr(), M, q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(),
                                         a2.data_ptr(), a2.numel(), y.data_ptr(), _lib.BF16, n, k, work.data_ptr(),
@@ -116,7 +131,7 @@ def main():
             rows["handoff"].append(s9 - s5)
             rows["end"].append(s9 - t0)
             spans.append(np.nanmax(s9) - t0)
-        out = {"variant": args.variant or "product", "cfg": cs or "library", "N": n, "K": k, "M": M, "waves_per_launch": int(len(rows["start"][0])),
+        out = {"variant": args.variant or "product", "chain": args.chain, "cfg": cs or "library", "N": n, "K": k, "M": M, "waves_per_launch": int(len(rows["start"][0])),
                "span_us": pct(spans)}
         for key, v in rows.items():
             out[key] = pct(np.concatenate(v))

@@ -94,6 +94,15 @@ def main():
             _s = (torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream())
         streams_us = (time.perf_counter() - h0) * 1e6 / args.iterations
         del _s
+        # the harness's own plumbing: the same loop with a dequant that returns a ready
+        # tensor (3 streams, 3 stream contexts, .t(), 3 wait_stream), no kernel
+        ready = torch.empty((2, 2), device="cuda")
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        for _ in range(args.iterations):
+            mlp_dequantize(mlp, lambda md: ready, sync=False)
+        plumbing_us = (time.perf_counter() - h0) * 1e6 / args.iterations
+        torch.cuda.synchronize()
         mods3 = [mlp.up_proj, mlp.gate_proj, mlp.down_proj]
         torch.cuda.synchronize()
         h0 = time.perf_counter()
@@ -138,6 +147,7 @@ def main():
                           "host_us_per_iteration_issue": host_loop_us,
                           "host_us_three_stream_creations": streams_us,
                           "host_us_three_dropin_calls_current_stream": calls_us,
+                          "host_us_harness_plumbing_no_kernel": plumbing_us,
                           "elements_per_iteration": elems}), flush=True)
         del outs, g
     # host cost of one API call (device work hidden behind a long queue)
