@@ -158,6 +158,14 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
 #endif
+//   NF4_DQ_FLUSH_EDGE   chunk kernel, LDS-staged stores (tools A/B, round 6): 0 (product);
+//                       1 = whole pieces in the span's first / last 128-byte line with the
+//                       default policy instead of nt; 2 = ablation, no end-piece element
+//                       stores (wrong outputs at span ends, timing only); 3 = every flush
+//                       store with the default policy
+#ifndef NF4_DQ_FLUSH_EDGE
+#define NF4_DQ_FLUSH_EDGE 0
+#endif
 
 constexpr int kWg = 256;   // rows / bitsandbytes-bytes kernels: 4 waves per workgroup
 constexpr int kFlatWaves = NF4_DQ_FLAT_WAVES;  // the flat kernel's workgroup
@@ -908,8 +916,21 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
                 if (x0 >= (int)span) break;
                 const bool whole = x0 >= 0 && x0 + 8 <= (int)span;
                 const u32x4 v = *reinterpret_cast<const u32x4_alias*>(stage + sbase + 16u * (lane + 64u * st));
-                __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxStore);
-                if (!whole) {
+                if constexpr (NF4_DQ_FLUSH_EDGE == 1) {
+                    // (tools A/B) the span's first / last line: default policy
+                    const uintptr_t ob = (uintptr_t)A.out + 2u * e0;
+                    const bool edge_line = ((ob + 2u * (uint32_t)x0) >> 7) == (ob >> 7) ||
+                                           ((ob + 2u * (uint32_t)x0) >> 7) == ((ob + 2u * span - 1u) >> 7);
+                    if (edge_line)
+                        __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxPiece);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxStore);
+                } else if constexpr (NF4_DQ_FLUSH_EDGE == 3) {
+                    __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxPiece);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxStore);
+                }
+                if (NF4_DQ_FLUSH_EDGE != 2 && !whole) {
 #pragma unroll
                     for (int i = 0; i < 8; ++i)
                         __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[i >> 1] >> (16 * (i & 1))), rsp,

@@ -18,6 +18,8 @@
 // gather delays (at 414c083), bitsandbytes-mode code-table loads and gather
 // delays (at 99ed841), and the chunk kernel's barrier / scale-gather placements (at 1601634).
 //   DQV_SINGLE=1   one-tile waves skip the pipelined loop
+//   DQV_FE=n   chunk kernel's LDS-staged flush (NF4_DQ_FLUSH_EDGE: 1 edge lines default policy,
+//              2 no end-piece element stores (timing only), 3 all flush stores default policy)
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
@@ -36,6 +38,9 @@
 #endif
 #ifdef DQV_SNT
 #define NF4_DQ_SCALE_NT DQV_SNT
+#endif
+#ifdef DQV_FE  // chunk kernel's staged flush (NF4_DQ_FLUSH_EDGE), round 6
+#define NF4_DQ_FLUSH_EDGE DQV_FE
 #endif
 
 #ifdef DQV_NOSCALE
