@@ -158,14 +158,6 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #ifndef NF4_DQ_ABL_NOSCALE
 #define NF4_DQ_ABL_NOSCALE 0
 #endif
-//   NF4_DQ_FLUSH_EDGE   chunk kernel, LDS-staged stores (tools A/B, round 6): 0 (product);
-//                       1 = whole pieces in the span's first / last 128-byte line with the
-//                       default policy instead of nt; 2 = ablation, no end-piece element
-//                       stores (wrong outputs at span ends, timing only); 3 = every flush
-//                       store with the default policy
-#ifndef NF4_DQ_FLUSH_EDGE
-#define NF4_DQ_FLUSH_EDGE 0
-#endif
 
 constexpr int kWg = 256;   // rows / bitsandbytes-bytes kernels: 4 waves per workgroup
 constexpr int kFlatWaves = NF4_DQ_FLAT_WAVES;  // the flat kernel's workgroup
@@ -905,37 +897,40 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             const uint32_t rl2 = fdiv(cl2, A.L);
             const uint32_t ql2 = cl2 - rl2 * A.L.d;
             const uint32_t span = (uint32_t)((uint64_t)rl2 * A.n + min(8u * ql2 + 8u, A.n) - e0);
-            // the span's own range: an end piece's elements outside it (another wave's) are
-            // dropped by the descriptor's range check -- below its start their offsets wrap
-            // past 2^31 -- so they need no compare each
-            const __amdgpu_buffer_rsrc_t rsp =
-                __builtin_amdgcn_make_buffer_rsrc((void*)((char*)A.out + e0 * 2u), 0, 2u * span, kRsrcFlags);
+            // Whole 16-byte pieces go out as one store each, nt -- except in the span's first
+            // and last 128-byte line, which the neighbouring wave writes too: those with the
+            // default policy, so that the L2 merges the two waves' parts of the line before it
+            // goes to HBM (round 6: 16.2 -> 14.4 us at 4096 x 4090, 15.3 -> 13.5 at 4095;
+            // profiles/r06/chunk/s3_flush_variants.jsonl).
+            const uintptr_t ob = (uintptr_t)A.out + 2u * e0;
+            const uintptr_t l_first = ob >> 7, l_last = (ob + 2u * span - 1u) >> 7;
 #pragma unroll
             for (int st = 0; st < 5; ++st) {
                 const int x0 = (int)(8u * (lane + 64u * st)) - (int)sa;  // piece k = lane + 64 st
                 if (x0 >= (int)span) break;
                 const bool whole = x0 >= 0 && x0 + 8 <= (int)span;
                 const u32x4 v = *reinterpret_cast<const u32x4_alias*>(stage + sbase + 16u * (lane + 64u * st));
-                if constexpr (NF4_DQ_FLUSH_EDGE == 1) {
-                    // (tools A/B) the span's first / last line: default policy
-                    const uintptr_t ob = (uintptr_t)A.out + 2u * e0;
-                    const bool edge_line = ((ob + 2u * (uint32_t)x0) >> 7) == (ob >> 7) ||
-                                           ((ob + 2u * (uint32_t)x0) >> 7) == ((ob + 2u * span - 1u) >> 7);
-                    if (edge_line)
-                        __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxPiece);
-                    else
-                        __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxStore);
-                } else if constexpr (NF4_DQ_FLUSH_EDGE == 3) {
-                    __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxPiece);
-                } else {
-                    __builtin_amdgcn_raw_buffer_store_b128(v, ro, whole ? 2u * (uint32_t)x0 : kDrop, 0, kAuxStore);
-                }
-                if (NF4_DQ_FLUSH_EDGE != 2 && !whole) {
+                const uint32_t off = whole ? 2u * (uint32_t)x0 : kDrop;
+                const uintptr_t l = (ob + 2u * (uint32_t)x0) >> 7;
+                if (l == l_first || l == l_last) __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, kAuxPiece);
+                else __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, kAuxStore);
+            }
+            // The span's two end pieces when they are not whole: lane 0 the first, lane 1 the
+            // last, element by element through the span's own range-checked descriptor -- the
+            // elements outside the span (the neighbour's) are dropped by the range check, below
+            // its start because their offsets wrap past 2^31 -- in ONE pass of 8 stores per wave
+            // (round 5 made a pass per end, each with a compare per element)
+            const __amdgpu_buffer_rsrc_t rsp =
+                __builtin_amdgcn_make_buffer_rsrc((void*)((char*)A.out + e0 * 2u), 0, 2u * span, kRsrcFlags);
+            const uint32_t klast = (span + sa - 1u) >> 3;
+            const uint32_t k = lane == 0u ? 0u : klast;
+            const int xe = (int)(8u * k) - (int)sa;
+            if (lane < 2u && (lane == 0u || klast != 0u) && !(xe >= 0 && xe + 8 <= (int)span)) {
+                const u32x4 v = *reinterpret_cast<const u32x4_alias*>(stage + sbase + 16u * k);
 #pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[i >> 1] >> (16 * (i & 1))), rsp,
-                                                              2u * (uint32_t)(x0 + i), 0, kAuxPiece);
-                }
+                for (int i = 0; i < 8; ++i)
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[i >> 1] >> (16 * (i & 1))), rsp,
+                                                          2u * (uint32_t)(xe + i), 0, kAuxPiece);
             }
         }
     };

@@ -19,7 +19,9 @@
 // delays (at 99ed841), and the chunk kernel's barrier / scale-gather placements (at 1601634).
 //   DQV_SINGLE=1   one-tile waves skip the pipelined loop
 //   DQV_FE=n   chunk kernel's LDS-staged flush (NF4_DQ_FLUSH_EDGE: 1 edge lines default policy,
-//              2 no end-piece element stores (timing only), 3 all flush stores default policy)
+//              2 no end-piece element stores (timing only), 3 all flush stores default policy);
+//              measured in round 6 (profiles/r06/chunk/s3_flush_variants.jsonl), the hook removed
+//              after measurement (it is in git history at effdce7)
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
