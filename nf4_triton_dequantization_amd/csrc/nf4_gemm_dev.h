@@ -1727,24 +1727,17 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     };
 
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, 0, A.M * A.K * 2u, kRsrcFlags);
-    // 1. x rows (the slice's K range), then round 0 of the ring.  Only the nx <= kXR
-    // iterations that hold pieces run (uniform branches): at M = 1 a 16-wave workgroup has
-    // one piece per thread, and the 7 dead iterations' address math (a division each) cost
-    // every wave ~60 VALU of prologue (round 6)
+    // 1. x rows (the slice's K range), then round 0 of the ring
     const uint32_t pieces = A.M * A.ppr.d;
-    const uint32_t nx = (pieces + 64u * W - 1u) / (64u * W);  // (host: <= kXR)
     u32x4 xv[kXR];
     uint32_t xdst[kXR];
 #pragma unroll
     for (int i = 0; i < kXR; ++i) {
-        xdst[i] = 0xFFFFFFFFu;
-        if ((uint32_t)i < nx) {
-            const uint32_t p = tid + (uint32_t)i * 64u * W;
-            const uint32_t r = fdiv(p, A.ppr), q = p - r * A.ppr.d;
-            xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, p < pieces ? r * A.K * 2u + cbase * 512u + q * 16u : kOob,
-                                                          0, 0);
-            xdst[i] = p < pieces ? kLdsX + r * A.xstride + q * 16u : 0xFFFFFFFFu;
-        }
+        const uint32_t p = tid + (uint32_t)i * 64u * W;
+        const uint32_t r = fdiv(p, A.ppr), q = p - r * A.ppr.d;
+        xv[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, p < pieces ? r * A.K * 2u + cbase * 512u + q * 16u : kOob,
+                                                      0, 0);
+        xdst[i] = p < pieces ? kLdsX + r * A.xstride + q * 16u : 0xFFFFFFFFu;
     }
     __builtin_amdgcn_sched_barrier(0);  // x loads first: the staging below must not wait on the ring
     PScales<P> sc[2];
@@ -1767,7 +1760,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     }
 #pragma unroll
     for (int i = 0; i < kXR; ++i)
-        if ((uint32_t)i < nx && xdst[i] != 0xFFFFFFFFu) *reinterpret_cast<u32x4*>(smem + xdst[i]) = xv[i];
+        if (xdst[i] != 0xFFFFFFFFu) *reinterpret_cast<u32x4*>(smem + xdst[i]) = xv[i];
     __syncthreads();
     NF4_GSTAMP(1);
 
