@@ -903,6 +903,26 @@ def test_check_gemm_workspaces_raises_on_a_set_error_word(coracle, gpu):
     assert check_gemm_workspaces() is None
 
 
+def test_release_gemm_workspaces_reports_a_pending_error(coracle, gpu):
+    """release_gemm_workspaces() reads each cached workspace's sticky error
+    word before forgetting it, so a split-K timeout since the last check is raised, not
+    lost -- and the cache is cleared either way."""
+    from nf4_triton_dequantization_amd import kernel, nf4_linear, release_gemm_workspaces
+
+    M, N, K = 16, 4096, 4096
+    packed, a1, a2 = O.make_inputs(N, K, seed=79)
+    mod = make_module(packed, a1, a2, N, K, "bf16", gpu)
+    xt, _ = _x_bits(M, K, "bf16", seed=5)
+    nf4_linear(xt.to(gpu), mod)
+    torch.cuda.synchronize()
+    key = (gpu.index if gpu.index is not None else 0, torch.cuda.current_stream(gpu).cuda_stream)
+    ws, _stream = kernel._GEMM_WS[key]
+    ws[65536] = 1  # the error word a reducer sets when its poll gives up
+    with pytest.raises(RuntimeError, match="split-K"):
+        release_gemm_workspaces()
+    assert not kernel._GEMM_WS
+
+
 def test_release_gemm_workspaces_empties_the_cache(gpu):
     """release_gemm_workspaces() synchronises the cached workspaces' streams and forgets
     them (for callers that destroy their own external streams); nf4_linear then builds a
