@@ -109,9 +109,6 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 #ifndef NF4_PERSIST_PAIR  // persistent kernel: two ring slots decoded step-interleaved (even P)
 #define NF4_PERSIST_PAIR 0
 #endif
-#ifndef NF4_PERSIST_CONT  // persistent kernel: one lookup pipeline across chunks (sslot_mma_cont)
-#define NF4_PERSIST_CONT 0
-#endif
 #ifndef NF4_ABL_LOOP_ON  // tools: persistent kernel skips its chunk loop (prologue + epilogue alone)
 #define NF4_ABL_LOOP_ON 1
 #endif
@@ -1397,63 +1394,6 @@ __device__ __forceinline__ void sslot_mma(const SSlot& s, uint32_t qa, float qb,
     }
 }
 
-// One chunk (one row tile) of a continuous lookup pipeline across chunks (round 6).  A
-// wave can hold at most 15 LDS operations in flight (lgkmcnt is 4 bits) and a step needs
-// 5 (4 pair lookups + the x fragment), so lookups run at most 3 steps ahead; sslot_mma
-// restarts that pipeline at every chunk (its first 3 steps' lookups go out together after
-// the chunk's weights arrive and the first MFMA waits a whole LDS round trip).  Here the
-// chunk's first 3 steps come looked up by the previous chunk (`pre`), and its last 3 steps
-// look up the first 3 of the next ring slot (`nx`; past the wave's last chunk the slot holds
-// out-of-range loads' zeros, so those lookups are harmless), so the lookups run 3 steps
-// ahead across chunk boundaries too.
-template <int DT>
-__device__ __forceinline__ void sslot_mma_cont(const SSlot& s, const SSlot& nx, float sc, const f32x2* ptab,
-                                               const char* smem, uint32_t slot8, uint32_t xa, f32x4& acc, f32x4& accb,
-                                               f32x2 (&pre)[3][4]) {
-    const f32x2 sc2 = {sc, opaque(sc)};
-    const char* pt = reinterpret_cast<const char*>(ptab);
-    constexpr int LA = 3;
-    f32x2 v[8][4];
-#pragma unroll
-    for (int st = 0; st < LA; ++st)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) v[st][b] = pre[st][b];
-    auto look = [&](uint32_t wd, f32x2 (&dst)[4]) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            dst[b] = NF4_ABL_LOOKUP(pt, __builtin_amdgcn_perm(wd, slot8, 0x0C0C0000u | ((4u + b) << 8)), wd);
-    };
-#pragma unroll
-    for (int st = 0; st < 8; ++st) {
-        if (st + LA < 8) {
-            const int sn = st + LA;
-            look(sn < 4 ? s.w0[sn] : s.w1[sn - 4], v[sn]);
-        } else {
-            const int sn = st + LA - 8;  // the next slot's first steps (its w0)
-            look(nx.w0[sn], pre[sn]);
-        }
-        const u32x4 a = *reinterpret_cast<const u32x4*>(smem + xa + 16u * st);
-        __builtin_amdgcn_sched_barrier(0);
-        uint32_t bw[4];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const f32x2 p = v[st][b] * sc2;  // fp32 products (:97-98)
-            bw[b] = pack2<DT>(p.x, p.y);     // RNE (:109-110)
-        }
-        const u32x4 bq = {bw[0], bw[1], bw[2], bw[3]};
-        f32x4& c = (st & 1) ? accb : acc;
-        if constexpr (!NF4_ABL_MMA_ON) {
-            asm volatile("" ::"v"(a), "v"(bq));
-        } else if constexpr (DT == NF4DQ_BF16) {
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, bq), c,
-                                                        0, 0, 0);
-        } else {
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, bq), c,
-                                                       0, 0, 0);
-        }
-    }
-}
-
 // Two chunks of one strip (one row tile, M <= 16) decoded step by step side by
 // side: two independent chains of pair lookups, x reads and MFMAs, so that one
 // chunk's LDS round trips overlap the other's VALU work.  Scales come in computed.
@@ -1829,16 +1769,6 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
     const uint32_t slot8 = (lane & 31u) * 8u;
     f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, accb[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
     uint32_t it = 0, rr = 0, buf = 0;
-    f32x2 pre[3][4];  // NF4_PERSIST_CONT: the next chunk's first 3 steps, looked up ahead
-    if constexpr (NF4_PERSIST_CONT) {
-        const char* pt = reinterpret_cast<const char*>(ptab);
-#pragma unroll
-        for (int st = 0; st < 3; ++st)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                pre[st][b] = NF4_ABL_LOOKUP(
-                    pt, __builtin_amdgcn_perm(ring[0].w0[st], slot8, 0x0C0C0000u | ((4u + b) << 8)), ring[0].w0[st]);
-    }
 
     auto round = [&](PScales<P>& cur, PScales<P>& nxt) {
         const bool more = it2 < mine;  // the issue pointer is one round ahead
@@ -1870,10 +1800,7 @@ __global__ __launch_bounds__(64 * W) void nf4_gemm_persist_kernel(const StreamAr
             for (int s = 0; s < P; ++s) {
                 const uint32_t l = l0 + rr * P + (uint32_t)s;
                 const uint32_t xa[1] = {live ? xa0 + l * 512u : xa0};
-                if constexpr (NF4_PERSIST_CONT)
-                    sslot_mma_cont<DT>(ring[s], ring[(s + 1) % P], scv[s], ptab, smem, slot8, xa[0], acc[0], accb[0], pre);
-                else
-                    sslot_mma<DT, 1, true>(ring[s], 0u, scv[s], ptab, qtab, smem, slot8, xa, acc, accb);
+                sslot_mma<DT, 1, true>(ring[s], 0u, scv[s], ptab, qtab, smem, slot8, xa, acc, accb);
                 if (it == 0 && rr == 0 && s == 0) NF4_GSTAMP(2);  // first chunk's weights arrived and consumed
                 __builtin_amdgcn_sched_barrier(0);
                 issue_w(ring[s], s, more);

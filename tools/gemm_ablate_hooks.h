@@ -5,9 +5,8 @@
 #if defined(ABL_NTW)  // weight loads with the nt (streaming) policy, as the flat dequant kernel's
 #define NF4_ABL_WLOAD(rsrc_, off_) __builtin_amdgcn_raw_buffer_load_b128((rsrc_), (off_), 0, 2)
 #endif
-#if defined(ABL_CONT)  // a variant, not an ablation: one lookup pipeline across chunks (round 6)
-#define NF4_PERSIST_CONT 1
-#endif
+// (ABL_CONT, round 6: one lookup pipeline across chunks -- measured slower at ring depth 2,
+// profiles/r06/gemm/s6_cont_pipeline_ab.jsonl; the variant is in git history at e7f9535)
 #if defined(ABL_PAIR)  // a variant, not an ablation: correct results
 #define NF4_PERSIST_PAIR 1
 #endif
