@@ -890,31 +890,53 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             }
         }
     };
-    auto flush16 = [&]() {
+    // The staged form's span: its length in elements and its first / last 128-byte line.
+    // Whole 16-byte pieces go out as one store each, nt -- except in those two lines, which
+    // the neighbouring wave writes too: those with the default policy, so that the L2 merges
+    // the two waves' parts of the line before it goes to HBM (round 6: 16.2 -> 14.4 us at
+    // 4096 x 4090, 15.3 -> 13.5 at 4095; profiles/r06/chunk/s3_flush_variants.jsonl).
+    uint32_t span = 0;
+    uintptr_t ob = 0, l_first = 0, l_last = 0;
+    if constexpr (SW != 16) {
+        const uint32_t cl2 = min(cw + 255u, A.chunks - 1u);
+        const uint32_t rl2 = fdiv(cl2, A.L);
+        const uint32_t ql2 = cl2 - rl2 * A.L.d;
+        span = cw >= A.chunks ? 0u : (uint32_t)((uint64_t)rl2 * A.n + min(8u * ql2 + 8u, A.n) - e0);
+        ob = (uintptr_t)A.out + 2u * e0;
+        l_first = ob >> 7;
+        l_last = (ob + 2u * span - 1u) >> 7;
+    }
+    // whole staged pieces k0 <= k < k1 (uniform bounds; piece k = elements 8k - sa .. + 7 of the span)
+    auto store_pieces = [&](uint32_t k0, uint32_t k1) {
+        for (uint32_t kb = k0; kb < k1; kb += 64u) {  // (uniform)
+            const uint32_t k = kb + lane;
+            const int x0 = (int)(8u * k) - (int)sa;
+            const bool whole = k < k1 && x0 >= 0 && x0 + 8 <= (int)span;
+            const u32x4 v = *reinterpret_cast<const u32x4_alias*>(stage + sbase + 16u * (k < k1 ? k : k0));
+            const uint32_t off = whole ? 2u * (uint32_t)x0 : kDrop;
+            const uintptr_t l = (ob + 2u * (uint32_t)x0) >> 7;
+            if (l == l_first || l == l_last) __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, kAuxPiece);
+            else __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, kAuxStore);
+        }
+    };
+    // after step j (rows of >= 64 chunks): every slot below the end of the step's last chunk
+    // (lane 63's) is final -- a past-n element lands only beyond its own chunk's last valid
+    // one -- so the pieces wholly below it can go out now, while later steps decode, instead
+    // of all after the last step (round 6)
+    auto flush_step = [&](int j, uint32_t& kdone) {
+        if constexpr (SW != 16) {
+            const uint32_t rel63 = __builtin_amdgcn_readlane(rel[j], 63);
+            const uint32_t col63 = __builtin_amdgcn_readlane(col[j], 63);
+            const uint32_t e_end = col63 < A.n ? rel63 + min(8u, A.n - col63) : span;
+            const uint32_t kmax = (e_end + sa) >> 3;
+            store_pieces(kdone, kmax);
+            kdone = kmax > kdone ? kmax : kdone;
+        }
+    };
+    auto flush16 = [&](uint32_t kdone) {
         if constexpr (SW != 16) {
             if (cw >= A.chunks) return;  // a wave wholly past the end stages nothing and writes nothing
-            const uint32_t cl2 = min(cw + 255u, A.chunks - 1u);
-            const uint32_t rl2 = fdiv(cl2, A.L);
-            const uint32_t ql2 = cl2 - rl2 * A.L.d;
-            const uint32_t span = (uint32_t)((uint64_t)rl2 * A.n + min(8u * ql2 + 8u, A.n) - e0);
-            // Whole 16-byte pieces go out as one store each, nt -- except in the span's first
-            // and last 128-byte line, which the neighbouring wave writes too: those with the
-            // default policy, so that the L2 merges the two waves' parts of the line before it
-            // goes to HBM (round 6: 16.2 -> 14.4 us at 4096 x 4090, 15.3 -> 13.5 at 4095;
-            // profiles/r06/chunk/s3_flush_variants.jsonl).
-            const uintptr_t ob = (uintptr_t)A.out + 2u * e0;
-            const uintptr_t l_first = ob >> 7, l_last = (ob + 2u * span - 1u) >> 7;
-#pragma unroll
-            for (int st = 0; st < 5; ++st) {
-                const int x0 = (int)(8u * (lane + 64u * st)) - (int)sa;  // piece k = lane + 64 st
-                if (x0 >= (int)span) break;
-                const bool whole = x0 >= 0 && x0 + 8 <= (int)span;
-                const u32x4 v = *reinterpret_cast<const u32x4_alias*>(stage + sbase + 16u * (lane + 64u * st));
-                const uint32_t off = whole ? 2u * (uint32_t)x0 : kDrop;
-                const uintptr_t l = (ob + 2u * (uint32_t)x0) >> 7;
-                if (l == l_first || l == l_last) __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, kAuxPiece);
-                else __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, kAuxStore);
-            }
+            store_pieces(kdone, (span + sa) >> 3);
             // The span's two end pieces when they are not whole: lane 0 the first, lane 1 the
             // last, element by element through the span's own range-checked descriptor -- the
             // elements outside the span (the neighbour's) are dropped by the range check, below
@@ -939,13 +961,15 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             // one table per block of the wave (chunk_table_build / chunk_table_decode)
             const uint32_t region = (threadIdx.x >> 6) << 11;
             chunk_table_build<DT>(ctbl, region, lane, sb);
+            uint32_t kdone = 0;  // staged pieces stored so far (uniform)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 uint32_t p[4];
                 chunk_table_decode(ctbl, region, w[j], gsel[j], p);
                 store16(j, p);
+                if (j < 3 && cw < A.chunks) flush_step(j, kdone);
             }
-            flush16();
+            flush16(kdone);
             return;
         }
     }
@@ -987,7 +1011,7 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
             store16(j, p);
         }
     }
-    if constexpr (DT != NF4DQ_F32) flush16();
+    if constexpr (DT != NF4DQ_F32) flush16(0u);
 }
 
 // Any length, bitsandbytes semantics: one thread per packed byte.
