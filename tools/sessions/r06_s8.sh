@@ -16,3 +16,6 @@ for i in 1 2; do
 done
 unset NF4DQ_LIB_PATH
 bash tools/session.sh r06_s8 gputest smoke bench20 rocprof pmc
+# the driver's exact command (CPU baseline included)
+timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 > $O/bench_driver_cmd.json 2> $O/bench_driver_cmd.err
+python3 -c "import json; d=json.load(open('$O/bench_driver_cmd.json')); print('driver cmd', round(d['ms_per_step']*1e3,3), round(d['roofline']['frac'],4), d['roofline'].get('frac_of_measured_copy'))"
