@@ -87,3 +87,41 @@ def big_samples(name: str):
     """(flat indices, expected bits) sampled from the reference output of a big golden case."""
     with np.load(os.path.join(GOLDEN, "big_samples.npz"), allow_pickle=False) as z:
         return z[name + "/idx"], z[name + "/bits"]
+
+
+# ---- sentinel-guarded device buffers (the chunk-kernel and past-the-end suites) ----
+GUARD = 64  # elements of sentinel before the output
+# and after it: wide, because a wave past the end of the matrix once wrote its (empty)
+# staged span at the element its unclamped row index pointed to, thousands of elements on
+GUARD_AFTER = 1 << 18
+
+
+def dev_bytes(a: np.ndarray, dev, offset=0):
+    """`a` on the device at byte `offset` (0..3) into a fresh allocation, and that allocation."""
+    import torch
+
+    big = torch.zeros(a.size + 8, dtype=torch.uint8, device=dev)
+    big[offset:offset + a.size] = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
+    return big, big.data_ptr() + offset
+
+
+def out_buffer(m, n, dt, dev, elem_offset):
+    """An output of m*n elements at `elem_offset` elements into a sentinel-filled buffer."""
+    import torch
+
+    buf = torch.full((GUARD + elem_offset + m * n + GUARD_AFTER,), float("nan"), dtype=torch_dtype(dt), device=dev)
+    bits = buf.view(torch.int32 if dt == "f32" else torch.int16)
+    bits.fill_(0x5A5A5A5A if dt == "f32" else 0x5A5A)
+    return buf, GUARD + elem_offset
+
+
+def check_guarded(buf, start, m, n, dt, want, what):
+    """The sentinels on both sides intact, and the output bit-equal to `want` ([m][n])."""
+    import torch
+
+    bits = buf.view(torch.int32 if dt == "f32" else torch.int16).cpu().numpy()
+    sentinel = 0x5A5A5A5A if dt == "f32" else 0x5A5A
+    assert (bits[:start] == sentinel).all(), f"{what}: write before the output"
+    assert (bits[start + m * n:] == sentinel).all(), f"{what}: write past the output"
+    got = bits[start:start + m * n].view(np.uint32 if dt == "f32" else np.uint16).reshape(m, n)
+    assert_bits_equal(got, want, dt, what)

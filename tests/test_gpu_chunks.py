@@ -24,45 +24,16 @@ import pytest
 import torch
 
 import nf4_oracle as O
-from _helpers import DT_CODE, assert_bits_equal, out_bits
+from _helpers import DT_CODE, assert_bits_equal, check_guarded as _check, dev_bytes as _dev_bytes, out_bits
+from _helpers import out_buffer as _out_buffer
 
 pytestmark = pytest.mark.gpu
-
-TORCH_DT = {"f16": torch.float16, "bf16": torch.bfloat16, "f32": torch.float32}
-GUARD = 64  # elements of sentinel before the output
-# and after it: wide, because a wave past the end of the matrix once wrote its (empty)
-# staged span at the element its unclamped row index pointed to, thousands of elements on
-GUARD_AFTER = 1 << 18
 
 
 def _lib():
     from nf4_triton_dequantization_amd import _lib
 
     return _lib
-
-
-def _dev_bytes(a: np.ndarray, dev, offset=0):
-    """`a` on the device at byte `offset` (0..3) into a fresh allocation, and that allocation."""
-    big = torch.zeros(a.size + 8, dtype=torch.uint8, device=dev)
-    big[offset:offset + a.size] = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
-    return big, big.data_ptr() + offset
-
-
-def _out_buffer(m, n, dt, dev, elem_offset):
-    """An output of m*n elements at `elem_offset` elements into a sentinel-filled buffer."""
-    buf = torch.full((GUARD + elem_offset + m * n + GUARD_AFTER,), float("nan"), dtype=TORCH_DT[dt], device=dev)
-    bits = buf.view(torch.int32 if dt == "f32" else torch.int16)
-    bits.fill_(0x5A5A5A5A if dt == "f32" else 0x5A5A)
-    return buf, GUARD + elem_offset
-
-
-def _check(buf, start, m, n, dt, want, what):
-    bits = buf.view(torch.int32 if dt == "f32" else torch.int16).cpu().numpy()
-    sentinel = 0x5A5A5A5A if dt == "f32" else 0x5A5A
-    assert (bits[:start] == sentinel).all(), f"{what}: write before the output"
-    assert (bits[start + m * n:] == sentinel).all(), f"{what}: write past the output"
-    got = bits[start:start + m * n].view(np.uint32 if dt == "f32" else np.uint16).reshape(m, n)
-    assert_bits_equal(got, want, dt, what)
 
 
 def _ref_call(dev, p, a1, a2, m, n, dt, p_off=0, o_elem_off=0, flags=None):

@@ -28,8 +28,7 @@ import pytest
 import torch
 
 import nf4_oracle as O
-from _helpers import DT_CODE
-from test_gpu_chunks import _check, _dev_bytes, _out_buffer
+from _helpers import DT_CODE, check_guarded as _check, dev_bytes as _dev_bytes, out_buffer as _out_buffer
 
 pytestmark = pytest.mark.gpu
 
