@@ -1014,6 +1014,188 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
     if constexpr (DT != NF4DQ_F32) flush16(0u);
 }
 
+// The piece kernel (round 6): the 16-bit outputs the chunk forms above can only store
+// through the LDS stage (n % 8 != 0, or the output off 16-byte alignment), for TIGHTLY
+// packed rows (exactly ceil(n / 2) bytes each: every bitsandbytes weight).  It works in
+// output order instead of chunk order: the output, from the 128-byte line holding its
+// first element, is cut into aligned 16-byte pieces of 8 elements, and lane i owns piece
+// 256 w + 64 j + i at step j of wave w.  So every whole piece is one nt 16-byte store
+// straight from registers and each output line is written by one wave -- no stage, no
+// line shared by two waves but the matrix's first and last.  The cost moves to the
+// loads, where it is cheap: element (r, c) is nibble 2 r ceil(n / 2) + c of the packed
+// stream (for even n the stream runs on across row ends, for odd n every row ends in a
+// pad nibble), so a piece starts at any nibble; the lane loads the two dwords around its
+// 5 bytes and forms the even and odd elements' code bytes with byte permutes and
+// rotates.  A piece can hold two scale blocks (a block boundary inside the row, or the
+// row's end: the next row's first block is the next block; rows whose last block is
+// shorter than 8 elements are left to the chunk kernel).  The per-block tables of 16
+// rounded outputs (as in the dense form) sit in 16 OVERLAPPING groups of 8 blocks --
+// group q holds blocks 4q .. 4q + 7 -- so both blocks of a piece lie in group tA / 4 and
+// one v_perm per element still forms its table address.
+struct PieceArgs {
+    const uint8_t* packed;  // the packed weight aligned down to 4 bytes
+    const uint8_t* a1;
+    const float* a2;
+    void* line;             // the output's first 128-byte line
+    void* out;
+    uint32_t prange;        // load range from `packed` (bytes)
+    uint32_t kb;            // the weight's first byte, from `packed` (0..3)
+    uint32_t sa;            // the output's first element, from `line` (0..63)
+    uint32_t elems;         // m * n
+    uint32_t n, half;       // columns; packed bytes per row = ceil(n / 2)
+    FastDiv nf, bpr;        // n; 64-column blocks per row
+    uint32_t groups;        // ceil(bpr / 4)
+    FastDiv nb, n2;         // ref: moduli of the absmax / nested-absmax indices
+    uint32_t rs;            // single: absmax per row
+};
+
+constexpr uint32_t kPieceTbl = 4096;  // a wave's tables: 16 groups x 8 blocks x 16 entries x 2 B
+
+template <int DT, int MODE, bool ODD>
+__global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
+    __shared__ __attribute__((aligned(256))) char ptbl[4 * kPieceTbl];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t kw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
+    if (8u * kw >= A.sa + A.elems) return;  // a wave wholly past the end (uniform; no barrier below)
+    // the wave's first element (< 0: wave 0, whose first pieces start before the output)
+    const int32_t fw = (int32_t)(8u * kw) - (int32_t)A.sa;
+    const uint32_t fwc = fw < 0 ? 0u : (uint32_t)fw;
+    const uint32_t r0 = fdiv(fwc, A.nf);
+    const uint32_t c0 = fwc - r0 * A.nf.d;
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.prange, kRsrcFlags);
+    // Each step's column (of the piece's first element; < 0 before the output) and rows
+    // past r0 (a step moves 512 elements, rows are >= 512: at most one row end per step),
+    // then the two dwords around the piece's nibbles -- all loads out first.
+    int32_t cj[4];
+    uint32_t dj[4], lo[4], hi[4];
+    int32_t bj[4];
+    {
+        int32_t c = (fw < 0 ? fw : (int32_t)c0) + 8 * (int32_t)lane;
+        uint32_t d = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j) c += 512;
+            if (c >= (int32_t)A.n) {
+                c -= (int32_t)A.n;
+                ++d;
+            }
+            cj[j] = c;
+            dj[j] = d;
+            // nibble 2 (kb + r ceil(n / 2)) + c, from `packed`; its byte (before the weight:
+            // negative, i.e. beyond the range once unsigned -- the load returns 0)
+            const int32_t b = (int32_t)(A.kb + (r0 + d) * A.half) + (c >> 1);
+            bj[j] = b;
+            const uint32_t a = (uint32_t)(b & ~3);
+            // the second dword's offset as its own register: folded into the instruction's
+            // offset field, a + 4 would be range-checked unwrapped, so the weight's first dword
+            // (a = -4) would read as 0 (the first piece of an output off its 128-byte line)
+            uint32_t a4 = a + 4u;
+            asm("" : "+v"(a4));
+            lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a, 0, 0);
+            hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a4, 0, 0);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // The wave's blocks are consecutive and at most 38: lane i rounds block g0 + i's table.
+    const uint32_t g0 = r0 * A.bpr.d + (c0 >> 6);
+    const uint32_t fl = min((uint32_t)(fw + 2047), A.elems - 1u);
+    const uint32_t rl = fdiv(fl, A.nf);
+    const uint32_t gl = rl * A.bpr.d + ((fl - rl * A.nf.d) >> 6);
+    float sb;
+    {
+        const uint32_t g = min(g0 + lane, gl);
+        const uint32_t r = fdiv(g, A.bpr);
+        const uint32_t b = g - r * A.bpr.d;
+        if constexpr (MODE == kRef) {
+            const float q8 = (float)A.a1[fmodu(g, A.nb)];
+            sb = (q8 / 127.0f) * A.a2[fmodu(opaque_mul(r, A.groups) + (b >> 2), A.n2)];  // IEEE division (:45, :270)
+        } else {
+            sb = A.a2[opaque_mul(r, A.rs) + b];
+        }
+    }
+    const uint32_t region = (threadIdx.x >> 6) * kPieceTbl;
+    {
+        uint32_t e[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            e[k] = pack2<DT>(__uint_as_float(kNf4Bits[2 * k]) * sb, __uint_as_float(kNf4Bits[2 * k + 1]) * sb);
+        // block i: slot i % 4 of group i / 4, and slot i % 4 + 4 of group i / 4 - 1
+        u32x4_alias* d0 = reinterpret_cast<u32x4_alias*>(ptbl + region + ((lane >> 2) << 8) + ((lane & 3u) << 5));
+        d0[0] = u32x4{e[0], e[1], e[2], e[3]};
+        d0[1] = u32x4{e[4], e[5], e[6], e[7]};
+        if (lane >= 4u) {
+            u32x4_alias* d1 = reinterpret_cast<u32x4_alias*>(ptbl + region + ((lane >> 2) << 8) - 256u + 128u +
+                                                            ((lane & 3u) << 5));
+            d1[0] = u32x4{e[0], e[1], e[2], e[3]};
+            d1[1] = u32x4{e[4], e[5], e[6], e[7]};
+        }
+    }
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(A.line, 0, 2u * (A.sa + A.elems), kRsrcFlags);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int32_t c = cj[j];
+        const bool neg = c < 0;  // (wave 0's first pieces: every element of block 0 or dropped)
+        const uint32_t cu = neg ? 0u : (uint32_t)c;
+        // the piece's first block, from g0, and the first element of the next block (8: none)
+        const uint32_t tA = min(dj[j] * A.bpr.d + (cu >> 6) - (c0 >> 6), 59u);  // (59: lanes past the end)
+        const bool straddle = !neg && cu + 8u > A.n;
+        const uint32_t ib = neg ? 8u : straddle ? A.n - cu : min(64u - (cu & 63u), 8u);
+        // elements 2i (E) and 2i + 1 (O) as code bytes: nibble c of the row is the high
+        // nibble of its byte when c is even.  W0 = bytes b .. b+3, W1 = b+1 .. b+4.
+        const uint32_t sel = 0x03020100u + 0x01010101u * (uint32_t)(bj[j] & 3);
+        const uint32_t w0 = __builtin_amdgcn_perm(hi[j], lo[j], sel);
+        const uint32_t w1 = __builtin_amdgcn_perm(hi[j], lo[j], sel + 0x01010101u);
+        const uint32_t h0 = __builtin_amdgcn_alignbit(w0, w0, 3u);   // high nibbles x 2 in bits 1..4
+        const uint32_t l0 = __builtin_amdgcn_alignbit(w0, w0, 31u);  // low nibbles x 2
+        const uint32_t h1 = __builtin_amdgcn_alignbit(w1, w1, 3u);
+        const bool odd = (c & 1) != 0;
+        uint32_t E = odd ? l0 : h0, O = odd ? h1 : l0;
+        // byte i of E is element 2i, of O element 2i + 1: bytes at or past element ib
+        const uint32_t mE = (uint32_t)(0xFFFFFFFF00000000ull >> (32u - 8u * ((ib + 1u) >> 1)));
+        const uint32_t mO = (uint32_t)(0xFFFFFFFF00000000ull >> (32u - 8u * (ib >> 1)));
+        if constexpr (ODD) {
+            // odd n: the elements past the row's end sit one nibble further on (the pad)
+            const uint32_t l1 = __builtin_amdgcn_alignbit(w1, w1, 31u);
+            const uint32_t E2 = O, O2 = odd ? l1 : h1;
+            const uint32_t s = straddle ? 0xFFFFFFFFu : 0u;
+            E = (E2 & (mE & s)) | (E & ~(mE & s));
+            O = (O2 & (mO & s)) | (O & ~(mO & s));
+        }
+        const uint32_t rep = (tA & 3u) * 0x20202020u;  // slot of block tA in its group, x 32
+        const uint32_t es = (E & 0x1E1E1E1Eu) | (rep + (mE & 0x20202020u));
+        const uint32_t os = (O & 0x1E1E1E1Eu) | (rep + (mO & 0x20202020u));
+        const uint32_t base = region + ((tA >> 2) << 8);
+        uint32_t p[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t ae = __builtin_amdgcn_perm(es, base, 0x03020104u + b);
+            const uint32_t ao = __builtin_amdgcn_perm(os, base, 0x03020104u + b);
+            const uint32_t ve = *reinterpret_cast<const u16_alias*>(ptbl + ae);
+            const uint32_t vo = *reinterpret_cast<const u16_alias*>(ptbl + ao);
+            p[b] = ve | (vo << 16);
+        }
+        const uint32_t k = kw + 64u * (uint32_t)j + lane;
+        const int32_t f = fw + 8 * (64 * j + (int32_t)lane);
+        const bool whole = f >= 0 && (uint32_t)f + 8u <= A.elems;
+        const u32x4 o = {p[0], p[1], p[2], p[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(o, ro, whole ? 16u * k : kDrop, 0, kAuxStore);
+        if (!whole && f < (int32_t)A.elems && f + 8 > 0) {
+            // the matrix's first or last piece, partly outside the output: element by element
+            // through the output's own range (offsets before it wrap past 2^31: dropped)
+            const __amdgpu_buffer_rsrc_t rsp =
+                __builtin_amdgcn_make_buffer_rsrc(A.out, 0, 2u * A.elems, kRsrcFlags);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                uint32_t oe = 2u * (uint32_t)(f + i);
+                asm("" : "+v"(oe));  // (each offset its own register: see a4 above)
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(p[i >> 1] >> (16 * (i & 1))), rsp, oe, 0,
+                                                      kAuxPiece);
+            }
+        }
+    }
+}
+
 // Any length, bitsandbytes semantics: one thread per packed byte.
 struct BnbBytesArgs {
     const uint8_t* packed;
@@ -1247,8 +1429,55 @@ void launch_chunks_lw(const ChunkArgs& A, int sw, unsigned g, hipStream_t st) {
     else hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 4>), dim3(g), dim3(kWg), 0, st, A);
 }
 
+// The piece kernel's shapes: 16-bit outputs the chunk forms would stage (n % 8 != 0, or
+// the output off 16-byte alignment), tightly packed rows, rows of >= 512 elements whose
+// last block holds >= 8 of them (a piece then touches at most two blocks and a step at
+// most one row end), and offsets below 2^31.
+bool piece_eligible(const ChunkArgs& A, int32_t dtype) {
+    const uint64_t half = (A.n + 1u) / 2u;
+    const uint64_t rows = A.out_elems / A.n;
+    return dtype != NF4DQ_F32 && !(A.n % 8u == 0 && aligned(A.out, 16)) && A.stride == half &&
+           A.packed_len == rows * half && A.n >= 512u && (A.n % 64u == 0 || A.n % 64u >= 8u) &&
+           2u * (A.out_elems + 64u) < (uint64_t(1) << 31) && A.packed_len + 8u < (uint64_t(1) << 31);
+}
+
+template <int MODE, int DT>
+void launch_pieces_dt(const PieceArgs& P, unsigned g, hipStream_t st) {
+    if (P.n & 1u) hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, true>), dim3(g), dim3(kWg), 0, st, P);
+    else hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, false>), dim3(g), dim3(kWg), 0, st, P);
+}
+
+template <int MODE>
+int launch_pieces(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
+    PieceArgs P{};
+    const uintptr_t pw = (uintptr_t)A.packed, ow = (uintptr_t)A.out;
+    P.packed = reinterpret_cast<const uint8_t*>(pw & ~uintptr_t(3));
+    P.kb = (uint32_t)(pw & 3u);
+    P.prange = (uint32_t)((P.kb + A.packed_len + 3u) & ~uint64_t(3));
+    P.a1 = A.a1;
+    P.a2 = A.a2;
+    P.out = A.out;
+    P.line = reinterpret_cast<void*>(ow & ~uintptr_t(127));
+    P.sa = (uint32_t)((ow & 127u) / 2u);
+    P.elems = (uint32_t)A.out_elems;
+    P.n = A.n;
+    P.half = (A.n + 1u) / 2u;
+    P.nf = make_fastdiv(A.n);
+    P.bpr = A.bpr;
+    P.groups = A.groups;
+    P.nb = A.nb;
+    P.n2 = A.n2;
+    P.rs = A.rs;
+    const uint32_t pieces = (P.sa + P.elems + 7u) / 8u;
+    const unsigned g = (pieces + 1023u) / 1024u;  // 4 waves x 256 pieces
+    if (dtype == NF4DQ_BF16) launch_pieces_dt<MODE, NF4DQ_BF16>(P, g, st);
+    else launch_pieces_dt<MODE, NF4DQ_F16>(P, g, st);
+    return hip_rc(hipGetLastError());
+}
+
 template <int MODE>
 int launch_chunks(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
+    if (piece_eligible(A, dtype)) return launch_pieces<MODE>(A, dtype, st);
     const unsigned g = (unsigned)((A.chunks + 1023u) / 1024u);  // 4 waves x 256 chunks
     if (dtype != NF4DQ_F32 && A.L.d >= 64u && A.stride == 4u * A.L.d && A.n % 8u == 0 && aligned(A.packed, 4) &&
         aligned(A.out, 16) && A.chunks < (1u << 27)) {

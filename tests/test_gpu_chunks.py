@@ -1,9 +1,13 @@
-"""The chunk kernels (``-m gpu``): every shape the flat kernel does not take.
+"""The chunk and piece kernels (``-m gpu``): every shape the flat kernel does not take.
 
-n % 64 != 0, padded packed rows and unaligned pointers go through the chunk kernels of
+n % 64 != 0, padded packed rows and unaligned pointers go through the kernels of
 csrc/nf4_dequant.hip.  Which instantiation a shape takes (launch_chunks):
 * nf4_chunk_dense_kernel -- 16-bit output, n % 8 == 0, packed rows of exactly 4 L bytes
   (L = chunks per row >= 64), 4-byte-aligned packed weight, 16-byte-aligned output;
+* nf4_piece_kernel -- 16-bit output the chunk kernel would stage (n % 8 != 0, or the
+  output off 16-byte alignment) when the packed rows are tight (exactly ceil(n / 2)
+  bytes), n >= 512 and the last block of a row holds >= 8 elements: aligned 16-byte
+  output pieces in output order, each from the two packed dwords around its nibbles;
 * nf4_chunk_kernel<LW, SW> otherwise, with the load form LW = 4 (dword loads: packed
   weight and row stride 4-byte aligned) or 1 (two aligned dwords per chunk joined with
   v_alignbyte: any alignment), and the store form SW = 16 (one 16-byte store per chunk,
@@ -63,8 +67,10 @@ CASES = [
     (37, 1000, 0, 0, 0),      # n % 8 == 0, rows of exactly 4 L bytes, L >= 64: the dense form
     (5, 4080, 0, 0, 0),       # (the dense form)
     (33, 1000, 4, 0, 0),      # padded rows: LW 4 (dword loads), SW 16 (16-byte chunk stores)
-    (9, 4080, 0, 0, 1),       # output off 16-byte alignment: LW 4, SW 4 (staged)
-    (9, 1002, 0, 0, 0),       # n % 8 == 2, stride 501: LW 1 (alignbyte pairs), SW 4 (staged)
+    (9, 4080, 0, 0, 1),       # output off 16-byte alignment, tight rows: the piece kernel (fp32: LW 4, SW 4)
+    (9, 4080, 4, 0, 1),       # the same with padded rows: LW 4, SW 4 (staged)
+    (9, 1002, 0, 0, 0),       # n % 8 == 2, stride 501: the piece kernel (fp32: LW 1, SW 4)
+    (9, 1002, 1, 0, 0),       # n % 8 == 2, padded to stride 502: LW 1, SW 4 (staged)
     (3, 6, 0, 0, 0),          # L = 1: LW 1, SW 4, per-step row division
     (7, 77, 0, 0, 0),         # odd n (stride 39): LW 1, SW 4
     (1, 1, 0, 0, 0),
@@ -74,10 +80,21 @@ CASES = [
     (6, 256, 2, 0, 0),        # n % 64 == 0 but padded: not flat (LW 1)
     (6, 256, 0, 1, 0),        # odd packed pointer: LW 1
     (6, 256, 0, 2, 1),        # output one element off 16-byte alignment: SW 4
-    (10, 1000, 0, 3, 3),      # LW 1, SW 4, L >= 64
+    (10, 1000, 0, 3, 3),      # piece kernel: odd packed address, output 3 elements off
+    (10, 1000, 2, 3, 3),      # the same, padded rows: LW 1, SW 4, L >= 64
     (3000, 2, 0, 0, 0),       # one chunk per row: 256 rows per wave (per-lane scale gathers)
     (300, 18, 5, 0, 1),
-    (129, 4100, 0, 0, 0),     # partial last wave
+    (129, 4100, 0, 0, 0),     # n % 64 == 4 (last block shorter than a piece): LW 4, SW 4, partial last wave
+    # the piece kernel: even n (the stream runs across row ends), odd n (a pad nibble per
+    # row), the shortest last block it takes (8: n % 64 == 8), n % 64 == 0 with the output
+    # off alignment, output offsets up to 63 elements into the first line, one row
+    (9, 4090, 0, 0, 0),
+    (9, 4095, 0, 0, 0),
+    (7, 1007, 0, 1, 37),
+    (5, 520, 0, 2, 63),
+    (6, 4096, 0, 3, 5),
+    (1, 600, 0, 0, 9),
+    (70, 521, 0, 0, 0),       # rows of 521 (last block of 9): a step crosses a row end in most lanes
 ]
 
 
@@ -100,7 +117,8 @@ def test_single_quant_chunk_kernel(coracle, gpu, dt):
     # index once ran past the absmax rows -- an out-of-range gather, seen by fuzz_api seed 61;
     # 37 x 1000 and 5 x 4080 unpadded: the dense form's kSingle scale gather)
     for (m, n, extra, pad) in ((12, 200, 0, 0), (6, 1002, 3, 1), (33, 77, 1, 0), (5, 4080, 2, 4), (48, 269, 0, 0),
-                               (51, 275, 2, 0), (122, 261, 1, 0), (37, 1000, 0, 0), (5, 4080, 1, 0)):
+                               (51, 275, 2, 0), (122, 261, 1, 0), (37, 1000, 0, 0), (5, 4080, 1, 0),
+                               (9, 4090, 0, 0), (7, 1007, 1, 0), (33, 521, 2, 0)):  # (the last three: piece kernel)
         stride = (n + 1) // 2 + pad
         p, _, _, single = O.golden_case_inputs(m, n, m + n, {"single": extra, "stride": stride})
         want = coracle.dequant_single(p, single, m, n, DT_CODE[dt])

@@ -6,11 +6,12 @@ its row index from its unclamped first chunk, gathered single-quant scales past 
 absmax rows and wrote its (empty) staged span past the output.  This module sweeps that
 class of shape on purpose, for every load / store form of the chunk kernels
 (csrc/nf4_dequant.hip: the dense form; the general form with dword loads or alignbyte
-dword pairs, whole-chunk 16-byte stores or LDS staging, rows of >= 64 chunks or fewer),
-in both scale modes:
+dword pairs, whole-chunk 16-byte stores or LDS staging, rows of >= 64 chunks or fewer)
+and of the piece kernel (16-bit outputs of tight rows in output order: even and odd n,
+odd packed and output offsets, the shortest last block it takes), in both scale modes:
 
-* m is chosen so that the last workgroup (4 waves x 256 four-byte chunks) holds 1, 2 and
-  3 waves wholly past the end, and 0 as the control;
+* m is chosen so that the last workgroup (4 waves x 256 four-byte chunks, or 256 16-byte
+  output pieces) holds 1, 2 and 3 waves wholly past the end, and 0 as the control;
 * the absmax arrays have exactly the length the matrix needs -- nb = m * blocks per row,
   n2 = m * nested groups per row, single-quant rows of exactly blocks-per-row entries --
   so no modulo wrap keeps a runaway index inside them;
@@ -32,16 +33,23 @@ from _helpers import DT_CODE, check_guarded as _check, dev_bytes as _dev_bytes, 
 
 pytestmark = pytest.mark.gpu
 
-# name: (n, extra packed bytes per row, packed byte offset, output element offset, dtypes)
+# name: (n, extra packed bytes per row, packed byte offset, output element offset, dtypes, kernel)
 FORMS = {
-    "dense": (1000, 0, 0, 0, ("bf16", "f16")),              # n % 8 == 0, rows of exactly 4 L bytes
-    "dword_whole": (1000, 4, 0, 0, ("bf16", "f32")),        # padded rows: dword loads, 16-byte stores
-    "alignbyte_whole": (1000, 0, 1, 0, ("f16", "f32")),     # odd packed address: dword pairs + v_alignbyte
-    "dword_staged": (1007, 0, 0, 0, ("bf16", "f16", "f32")),  # n % 8 == 7, stride 504: LDS-staged stores
-    "alignbyte_staged": (1002, 0, 0, 0, ("bf16", "f32")),   # n % 8 == 2, stride 501: both at once
-    "unaligned_out": (1000, 0, 0, 1, ("bf16",)),            # output one element off 16 bytes: staged
-    "short_rows": (200, 0, 0, 0, ("bf16", "f32")),          # L = 25 < 64 chunks: per-step row division
-    "short_odd": (77, 0, 0, 0, ("f16",)),                   # L = 10, odd n: staged, dword pairs
+    "dense": (1000, 0, 0, 0, ("bf16", "f16"), "chunk"),              # n % 8 == 0, rows of exactly 4 L bytes
+    "dword_whole": (1000, 4, 0, 0, ("bf16", "f32"), "chunk"),        # padded rows: dword loads, 16-byte stores
+    "alignbyte_whole": (1000, 0, 1, 0, ("f16", "f32"), "chunk"),     # odd packed address: dword pairs + v_alignbyte
+    "dword_staged": (1007, 4, 0, 0, ("bf16", "f16", "f32"), "chunk"),  # padded odd-n rows (stride 508): LDS-staged
+    "alignbyte_staged": (1029, 0, 0, 0, ("bf16", "f32"), "chunk"),   # last block of 5 elements, stride 515: both
+    "unaligned_out": (1000, 4, 0, 1, ("bf16",), "chunk"),            # padded rows, output one element off: staged
+    "short_rows": (200, 0, 0, 0, ("bf16", "f32"), "chunk"),          # L = 25 < 64 chunks: per-step row division
+    "short_odd": (77, 0, 0, 0, ("f16",), "chunk"),                   # L = 10, odd n: staged, dword pairs
+    "tight_f32": (1007, 0, 0, 0, ("f32",), "chunk"),                 # fp32 of a piece-kernel shape: element stores
+    # the piece kernel (16-bit output, tight rows, n % 8 != 0 or the output off 16 bytes):
+    "piece_even": (1002, 0, 0, 0, ("bf16", "f16"), "piece"),         # the stream runs on across row ends
+    "piece_odd": (1007, 0, 0, 0, ("bf16", "f16"), "piece"),          # a pad nibble at every row end
+    "piece_offsets": (1007, 0, 1, 37, ("bf16",), "piece"),           # odd packed address, output 37 elements in
+    "piece_aligned_n": (1000, 0, 0, 1, ("f16",), "piece"),           # n % 8 == 0, output one element off
+    "piece_min_block": (520, 0, 3, 5, ("bf16",), "piece"),           # last block of 8 elements, rows of 520
 }
 
 
@@ -49,14 +57,22 @@ def _chunks_per_row(n):
     return ((n + 1) // 2 + 3) // 4
 
 
-def _m_with_past_end_waves(L, k, m0=1):
+def _units(form, m):
+    """256 of these per wave: 4-byte packed chunks (chunk kernels) or 16-byte output pieces
+    from the output's 128-byte line (the piece kernel; torch allocations are 128-aligned and
+    the sentinel is 64 elements, so the output sits `ooff` elements into its line)."""
+    n, _, _, ooff, _, kind = FORMS[form]
+    return m * _chunks_per_row(n) if kind == "chunk" else -(-(ooff + m * n) // 8)
+
+
+def _m_with_past_end_waves(form, k, m0=1):
     """Smallest m >= m0 whose last workgroup holds exactly k waves wholly past the end."""
     for m in range(m0, 1 << 14):
-        chunks = m * L
-        waves = -(-chunks // 256)
-        if 4 * -(-chunks // 1024) - waves == k:
+        units = _units(form, m)
+        waves = -(-units // 256)
+        if 4 * -(-units // 1024) - waves == k:
             return m
-    raise AssertionError((L, k))
+    raise AssertionError((form, k))
 
 
 def _exact_absmax(m, n, seed):
@@ -72,8 +88,8 @@ def test_chunk_forms_with_waves_past_the_end(coracle, gpu, form, past, m0):
     from nf4_triton_dequantization_amd import _lib
 
     L = _lib.lib()
-    n, pad, poff, ooff, dts = FORMS[form]
-    m = _m_with_past_end_waves(_chunks_per_row(n), past, m0)
+    n, pad, poff, ooff, dts, _ = FORMS[form]
+    m = _m_with_past_end_waves(form, past, m0)
     seed = 7 * m + n + past
     ov, bpr = _exact_absmax(m, n, seed)
     stride = (n + 1) // 2 + pad
@@ -84,6 +100,7 @@ def test_chunk_forms_with_waves_past_the_end(coracle, gpu, form, past, m0):
     t1, t2, ts = (torch.from_numpy(a).to(gpu) for a in (a1, a2, single))
     for dt in dts:
         buf, start = _out_buffer(m, n, dt, gpu, ooff)
+        assert buf.data_ptr() % 128 == 0  # (the piece count above assumes it)
         optr = buf.data_ptr() + start * buf.element_size()
         rc = L.nf4_dequant_ref(pp, p.size, t1.data_ptr(), t1.numel(), t2.data_ptr(), t2.numel(), optr, DT_CODE[dt],
                                m, n, st)

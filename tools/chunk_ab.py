@@ -13,6 +13,7 @@ launches behind a spin, as bench.py times its steps):
   chunk_4090    4096x4090 (n % 8 == 2: 4-byte stores)
   pad_4096      4096x4096 with packed rows of 2052 bytes (the general form, dword loads)
   unal_4096     4096x4096 with the packed weight at an odd address (byte loads)
+  oal_4096      4096x4096 with the output one element off 16-byte alignment
 --libs a,b: the same cases through other builds of the library (tools/_build/libnf4dq_<x>.so),
 interleaved, tagged "<x>:<case>".
 Prints one JSON line per case: median / min / max us per launch and the fraction of
@@ -37,16 +38,17 @@ from bench_configs import PEAK, alg_bytes, rotating_sets, rotation  # noqa: E402
 SHAPES = {"flat_4096": (4096, 4096, 0), "chunk_4096": (4096, 4096, _lib.CFG_CHUNKS),
           "chunk_4080": (4096, 4080, 0), "rows_4080": (4096, 4080, _lib.CFG_ROWS),
           "chunk_4095": (4096, 4095, 0), "chunk_4090": (4096, 4090, 0),
-          "pad_4096": (4096, 4096, 0), "unal_4096": (4096, 4096, 0)}
+          "pad_4096": (4096, 4096, 0), "unal_4096": (4096, 4096, 0), "oal_4096": (4096, 4096, 0)}
 # pad_4096: packed rows of 2052 bytes (n % 64 == 0 but not dense: the general form with
 # dword loads); unal_4096: the packed weight one byte into its allocation (alignbyte loads)
 PAD = {"pad_4096": 4}
 UNAL = {"unal_4096": 1}
+OOFF = {"oal_4096": 1}  # output element offset
 
 
 def case_key(name):
     m, n, _ = SHAPES[name]
-    return (m, n, PAD.get(name, 0), UNAL.get(name, 0))
+    return (m, n, PAD.get(name, 0), UNAL.get(name, 0), OOFF.get(name, 0))
 
 
 def case_sets(name, dev, gen):
@@ -55,7 +57,7 @@ def case_sets(name, dev, gen):
     m, n, _ = SHAPES[name]
     key = case_key(name)
     pin, pout = rotation(m, n, 2)
-    if n % 2 or key[2] or key[3]:  # packed rows of ceil(n/2) + pad bytes, at byte offset unal
+    if n % 2 or key[2] or key[3] or key[4]:  # packed rows of ceil(n/2) + pad bytes, at byte offset unal
         ins = []
         stride = (n + 1) // 2 + key[2]
         for _ in range(pin):
@@ -64,7 +66,7 @@ def case_sets(name, dev, gen):
             ins.append((q[key[3]:],
                         torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen),
                         torch.rand((nb + 255) // 256, device=dev, generator=gen) * 0.01 + 1e-3))
-        outs = [torch.empty((m, n), dtype=torch.bfloat16, device=dev) for _ in range(pout)]
+        outs = [torch.empty((m * n + 64,), dtype=torch.bfloat16, device=dev)[key[4]:] for _ in range(pout)]
         return ins, outs
     return rotating_sets(m, n, torch.bfloat16, dev, gen, pin, pout)
 
@@ -105,7 +107,7 @@ def main():
         lname, name = tag.split(":")
         L = libs[lname]
         m, n, flags = SHAPES[name]
-        ins, outs = sets[(m, n, PAD.get(name, 0), UNAL.get(name, 0))]
+        ins, outs = sets[case_key(name)]
 
         def launch(i):
             q, a1, a2 = ins[i % len(ins)]
@@ -124,7 +126,7 @@ def main():
     fns = {nm: launcher(nm) for nm in names}
     for nm in names:  # every set touched once
         c = nm.split(":")[1]
-        ins, outs = sets[SHAPES[c][:2] + (PAD.get(c, 0), UNAL.get(c, 0))]
+        ins, outs = sets[case_key(c)]
         for i in range(max(len(ins), len(outs))):
             fns[nm](i)
     torch.cuda.synchronize()

@@ -110,7 +110,7 @@ def main():
         p, a1, a2, _ = O.golden_case_inputs(m, n, seed, ov)
         want = orc.dequant_ref(p, a1, a2, m, n, DT[dt])
         if rng.random() < args.abi_rate:
-            poff, ooff = int(rng.integers(0, 4)), int(rng.integers(0, 8))
+            poff, ooff = int(rng.integers(0, 4)), int(rng.integers(0, 64))
             ov = dict(ov, packed_offset=poff, out_offset=ooff)
             ok = abi_case(dev, p, a1, a2, m, n, dt, poff, ooff, want)
         else:
