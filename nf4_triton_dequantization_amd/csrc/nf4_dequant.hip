@@ -1051,6 +1051,10 @@ struct PieceArgs {
 
 constexpr uint32_t kPieceTbl = 4096;  // a wave's tables: 16 groups x 8 blocks x 16 entries x 2 B
 
+// byte 0 of x in all four bytes (one v_perm_b32; a multiply by 0x01010101 is a quarter-rate
+// v_mul_lo_u32, and the constant does not fit v_mul_u32_u24's 24 bits)
+__device__ __forceinline__ uint32_t bytes4(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0u); }
+
 template <int DT, int MODE, bool ODD>
 __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
     __shared__ __attribute__((aligned(256))) char ptbl[4 * kPieceTbl];
@@ -1066,24 +1070,24 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
     // Each step's column (of the piece's first element; < 0 before the output) and rows
     // past r0 (a step moves 512 elements, rows are >= 512: at most one row end per step),
     // then the two dwords around the piece's nibbles -- all loads out first.
-    int32_t cj[4];
-    uint32_t dj[4], lo[4], hi[4];
-    int32_t bj[4];
+    int32_t cj[4], bj[4];
+    uint32_t gj[4], lo[4], hi[4];
     {
         int32_t c = (fw < 0 ? fw : (int32_t)c0) + 8 * (int32_t)lane;
-        uint32_t d = 0;
+        uint32_t pb = A.kb + r0 * A.half;  // the row's first packed byte, from `packed`
+        uint32_t gb = 0u - (c0 >> 6);       // the row's first block, from g0 (below)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (j) c += 512;
-            if (c >= (int32_t)A.n) {
-                c -= (int32_t)A.n;
-                ++d;
-            }
+            const bool wrap = c >= (int32_t)A.n;  // (additions only: no multiply per step)
+            c = wrap ? c - (int32_t)A.n : c;
+            pb = wrap ? pb + A.half : pb;
+            gb = wrap ? gb + A.bpr.d : gb;
             cj[j] = c;
-            dj[j] = d;
-            // nibble 2 (kb + r ceil(n / 2)) + c, from `packed`; its byte (before the weight:
-            // negative, i.e. beyond the range once unsigned -- the load returns 0)
-            const int32_t b = (int32_t)(A.kb + (r0 + d) * A.half) + (c >> 1);
+            gj[j] = gb;
+            // the byte holding nibble c of the row (before the weight: negative, i.e. beyond
+            // the range once unsigned -- the load returns 0)
+            const int32_t b = (int32_t)pb + (c >> 1);
             bj[j] = b;
             const uint32_t a = (uint32_t)(b & ~3);
             // the second dword's offset as its own register: folded into the instruction's
@@ -1135,15 +1139,21 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int32_t c = cj[j];
-        const bool neg = c < 0;  // (wave 0's first pieces: every element of block 0 or dropped)
-        const uint32_t cu = neg ? 0u : (uint32_t)c;
-        // the piece's first block, from g0, and the first element of the next block (8: none)
-        const uint32_t tA = min(dj[j] * A.bpr.d + (cu >> 6) - (c0 >> 6), 59u);  // (59: lanes past the end)
-        const bool straddle = !neg && cu + 8u > A.n;
-        const uint32_t ib = neg ? 8u : straddle ? A.n - cu : min(64u - (cu & 63u), 8u);
+        // (c < 0: wave 0's first pieces, whose elements are block 0's or dropped)
+        const uint32_t cu = (uint32_t)max(c, 0);
+        // the piece's first block (from g0) and the first element of the next block, if any
+        // (8: none): a boundary inside the row or the row's end, whichever comes first --
+        // the row end, when inside the piece, is the first (the last block holds >= 8)
+        const uint32_t tA = min(gj[j] + (cu >> 6), 59u);  // (59: lanes past the end)
+        const uint32_t ib = min(min(64u - (cu & 63u), A.n - cu), 8u);
+        // byte i of E is element 2i, of O element 2i + 1; bit 5 of each byte of yE / yO: the
+        // element lies at or past ib (0x80 + 2i - ib >= 0x80, bytes never borrow)
+        const uint32_t ibr = bytes4(ib);
+        const uint32_t yE = ((0x86848280u - ibr) >> 2) & 0x20202020u;
+        const uint32_t yO = ((0x87858381u - ibr) >> 2) & 0x20202020u;
         // elements 2i (E) and 2i + 1 (O) as code bytes: nibble c of the row is the high
         // nibble of its byte when c is even.  W0 = bytes b .. b+3, W1 = b+1 .. b+4.
-        const uint32_t sel = 0x03020100u + 0x01010101u * (uint32_t)(bj[j] & 3);
+        const uint32_t sel = bytes4((uint32_t)bj[j] & 3u) + 0x03020100u;
         const uint32_t w0 = __builtin_amdgcn_perm(hi[j], lo[j], sel);
         const uint32_t w1 = __builtin_amdgcn_perm(hi[j], lo[j], sel + 0x01010101u);
         const uint32_t h0 = __builtin_amdgcn_alignbit(w0, w0, 3u);   // high nibbles x 2 in bits 1..4
@@ -1151,20 +1161,19 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
         const uint32_t h1 = __builtin_amdgcn_alignbit(w1, w1, 3u);
         const bool odd = (c & 1) != 0;
         uint32_t E = odd ? l0 : h0, O = odd ? h1 : l0;
-        // byte i of E is element 2i, of O element 2i + 1: bytes at or past element ib
-        const uint32_t mE = (uint32_t)(0xFFFFFFFF00000000ull >> (32u - 8u * ((ib + 1u) >> 1)));
-        const uint32_t mO = (uint32_t)(0xFFFFFFFF00000000ull >> (32u - 8u * (ib >> 1)));
         if constexpr (ODD) {
             // odd n: the elements past the row's end sit one nibble further on (the pad)
             const uint32_t l1 = __builtin_amdgcn_alignbit(w1, w1, 31u);
             const uint32_t E2 = O, O2 = odd ? l1 : h1;
-            const uint32_t s = straddle ? 0xFFFFFFFFu : 0u;
-            E = (E2 & (mE & s)) | (E & ~(mE & s));
-            O = (O2 & (mO & s)) | (O & ~(mO & s));
+            const bool straddle = A.n - cu < 8u;
+            const uint32_t kE = straddle ? yE - (yE >> 4) : 0u;  // 0x1E in the bytes past the end
+            const uint32_t kO = straddle ? yO - (yO >> 4) : 0u;
+            E = (E2 & kE) | (E & ~kE);
+            O = (O2 & kO) | (O & ~kO);
         }
-        const uint32_t rep = (tA & 3u) * 0x20202020u;  // slot of block tA in its group, x 32
-        const uint32_t es = (E & 0x1E1E1E1Eu) | (rep + (mE & 0x20202020u));
-        const uint32_t os = (O & 0x1E1E1E1Eu) | (rep + (mO & 0x20202020u));
+        const uint32_t rep = bytes4((tA << 5) & 0x60u);  // slot of block tA in its group, x 32
+        const uint32_t es = (E & 0x1E1E1E1Eu) | (rep + yE);
+        const uint32_t os = (O & 0x1E1E1E1Eu) | (rep + yO);
         const uint32_t base = region + ((tA >> 2) << 8);
         uint32_t p[4];
 #pragma unroll

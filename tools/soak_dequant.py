@@ -89,7 +89,9 @@ def main():
     forms = [Form("flat_bf16", 4096, 4096, O.BF16, dev, orc, 11), Form("flat_f16", 4096, 4096, O.F16, dev, orc, 12),
              Form("flat_f32", 4096, 4096, O.F32, dev, orc, 13), Form("dense_bf16", 4096, 4080, O.BF16, dev, orc, 14),
              Form("padded_bf16", 1024, 4096, O.BF16, dev, orc, 15, pad=4),
-             Form("odd_f16", 777, 4095, O.F16, dev, orc, 16, ooff=3),
+             Form("odd_f16", 777, 4095, O.F16, dev, orc, 16, ooff=3),          # the piece kernel
+             Form("piece_even_bf16", 1024, 4090, O.BF16, dev, orc, 19, poff=2, ooff=45),
+             Form("staged_f16", 777, 4095, O.F16, dev, orc, 20, pad=3, ooff=3),  # LDS-staged chunk form
              Form("unaligned_bf16", 513, 1000, O.BF16, dev, orc, 17, poff=1, ooff=1),
              Form("single_bf16", 1000, 4080, O.BF16, dev, orc, 18, single=True)]
     # one Llama-3-8B layer through the batched entry (flat pieces in one launch)
