@@ -159,6 +159,7 @@ __device__ __forceinline__ void store1(void* out, int64_t i, float x) {
 #define NF4_DQ_ABL_NOSCALE 0
 #endif
 
+
 constexpr int kWg = 256;   // rows / bitsandbytes-bytes kernels: 4 waves per workgroup
 constexpr int kFlatWaves = NF4_DQ_FLAT_WAVES;  // the flat kernel's workgroup
 constexpr int kFlatWg = 64 * kFlatWaves;
@@ -1071,7 +1072,7 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
     // past r0 (a step moves 512 elements, rows are >= 512: at most one row end per step),
     // then the two dwords around the piece's nibbles -- all loads out first.
     int32_t cj[4], bj[4];
-    uint32_t gj[4], lo[4], hi[4];
+    uint32_t gj[4], aj[4], lo[4], hi[4];
     {
         int32_t c = (fw < 0 ? fw : (int32_t)c0) + 8 * (int32_t)lane;
         uint32_t pb = A.kb + r0 * A.half;  // the row's first packed byte, from `packed`
@@ -1089,15 +1090,20 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
             // the range once unsigned -- the load returns 0)
             const int32_t b = (int32_t)pb + (c >> 1);
             bj[j] = b;
-            const uint32_t a = (uint32_t)(b & ~3);
-            // the second dword's offset as its own register: folded into the instruction's
-            // offset field, a + 4 would be range-checked unwrapped, so the weight's first dword
-            // (a = -4) would read as 0 (the first piece of an output off its 128-byte line)
-            uint32_t a4 = a + 4u;
-            asm("" : "+v"(a4));
-            lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a, 0, 0);
-            hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a4, 0, 0);
+            aj[j] = (uint32_t)(b & ~3);
         }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        // the second dword's offset as its own register: folded into the instruction's offset
+        // field (or the pair merged into one 8-byte load), a + 4 would be range-checked
+        // unwrapped, so the weight's first dword (a = -4) would read as 0 (the first piece of
+        // an output off its 128-byte line).  (8-byte loads for the waves past the first line:
+        // 5-13 % slower, round 6 s14.)
+        uint32_t a4 = aj[j] + 4u;
+        asm("" : "+v"(a4));
+        lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, aj[j], 0, 0);
+        hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a4, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
     // The wave's blocks are consecutive and at most 38: lane i rounds block g0 + i's table.
@@ -1182,7 +1188,7 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
             const uint32_t ao = __builtin_amdgcn_perm(os, base, 0x03020104u + b);
             const uint32_t ve = *reinterpret_cast<const u16_alias*>(ptbl + ae);
             const uint32_t vo = *reinterpret_cast<const u16_alias*>(ptbl + ao);
-            p[b] = ve | (vo << 16);
+            p[b] = __builtin_amdgcn_perm(vo, ve, 0x05040100u);  // (one v_perm; the compiler made shift + or_sdwa)
         }
         const uint32_t k = kw + 64u * (uint32_t)j + lane;
         const int32_t f = fw + 8 * (64 * j + (int32_t)lane);

@@ -22,6 +22,9 @@
 //              2 no end-piece element stores (timing only), 3 all flush stores default policy);
 //              measured in round 6 (profiles/r06/chunk/s3_flush_variants.jsonl), the hook removed
 //              after measurement (it is in git history at effdce7)
+//   DQV_LD64=1 the piece kernel's 8-byte packed loads (NF4_DQ_PIECE_LD64): 5-13 % slower in
+//              round 6 (profiles/r06/chunk/s14_piece_ld64_ab.jsonl); the hook removed after
+//              measurement (in git history at the commit that adds that file)
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
