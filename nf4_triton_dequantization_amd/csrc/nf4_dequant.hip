@@ -1444,14 +1444,20 @@ void launch_chunks_lw(const ChunkArgs& A, int sw, unsigned g, hipStream_t st) {
     else hipLaunchKernelGGL((nf4_chunk_kernel<DT, MODE, LW, 4>), dim3(g), dim3(kWg), 0, st, A);
 }
 
-// The piece kernel's shapes: 16-bit outputs the chunk forms would stage (n % 8 != 0, or
-// the output off 16-byte alignment), tightly packed rows, rows of >= 512 elements whose
-// last block holds >= 8 of them (a piece then touches at most two blocks and a step at
-// most one row end), and offsets below 2^31.
+// The dense form's shapes (checked first).
+bool dense_eligible(const ChunkArgs& A, int32_t dtype) {
+    return dtype != NF4DQ_F32 && A.L.d >= 64u && A.stride == 4u * A.L.d && A.n % 8u == 0 && aligned(A.packed, 4) &&
+           aligned(A.out, 16) && A.chunks < (1u << 27);
+}
+
+// The piece kernel's shapes: 16-bit outputs of tightly packed rows the dense form does not
+// take (n % 8 != 0, the output off 16-byte alignment, or the packed weight off 4-byte
+// alignment), rows of >= 512 elements whose last block holds >= 8 of them (a piece then
+// touches at most two blocks and a step at most one row end), and offsets below 2^31.
 bool piece_eligible(const ChunkArgs& A, int32_t dtype) {
     const uint64_t half = (A.n + 1u) / 2u;
     const uint64_t rows = A.out_elems / A.n;
-    return dtype != NF4DQ_F32 && !(A.n % 8u == 0 && aligned(A.out, 16)) && A.stride == half &&
+    return dtype != NF4DQ_F32 && A.stride == half &&
            A.packed_len == rows * half && A.n >= 512u && (A.n % 64u == 0 || A.n % 64u >= 8u) &&
            2u * (A.out_elems + 64u) < (uint64_t(1) << 31) && A.packed_len + 8u < (uint64_t(1) << 31);
 }
@@ -1492,10 +1498,9 @@ int launch_pieces(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
 
 template <int MODE>
 int launch_chunks(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
-    if (piece_eligible(A, dtype)) return launch_pieces<MODE>(A, dtype, st);
     const unsigned g = (unsigned)((A.chunks + 1023u) / 1024u);  // 4 waves x 256 chunks
-    if (dtype != NF4DQ_F32 && A.L.d >= 64u && A.stride == 4u * A.L.d && A.n % 8u == 0 && aligned(A.packed, 4) &&
-        aligned(A.out, 16) && A.chunks < (1u << 27)) {
+    if (!dense_eligible(A, dtype) && piece_eligible(A, dtype)) return launch_pieces<MODE>(A, dtype, st);
+    if (dense_eligible(A, dtype)) {
         if (dtype == NF4DQ_BF16) hipLaunchKernelGGL((nf4_chunk_dense_kernel<NF4DQ_BF16, MODE>), dim3(g), dim3(kWg), 0, st, A);
         else hipLaunchKernelGGL((nf4_chunk_dense_kernel<NF4DQ_F16, MODE>), dim3(g), dim3(kWg), 0, st, A);
         return hip_rc(hipGetLastError());

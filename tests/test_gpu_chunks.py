@@ -4,10 +4,11 @@ n % 64 != 0, padded packed rows and unaligned pointers go through the kernels of
 csrc/nf4_dequant.hip.  Which instantiation a shape takes (launch_chunks):
 * nf4_chunk_dense_kernel -- 16-bit output, n % 8 == 0, packed rows of exactly 4 L bytes
   (L = chunks per row >= 64), 4-byte-aligned packed weight, 16-byte-aligned output;
-* nf4_piece_kernel -- 16-bit output the chunk kernel would stage (n % 8 != 0, or the
-  output off 16-byte alignment) when the packed rows are tight (exactly ceil(n / 2)
-  bytes), n >= 512 and the last block of a row holds >= 8 elements: aligned 16-byte
-  output pieces in output order, each from the two packed dwords around its nibbles;
+* nf4_piece_kernel -- 16-bit output of tight packed rows (exactly ceil(n / 2) bytes) that
+  the dense form does not take (n % 8 != 0, the output off 16-byte alignment or the
+  packed weight off 4-byte alignment), n >= 512, the last block of a row >= 8 elements:
+  aligned 16-byte output pieces in output order, each from the two packed dwords around
+  its nibbles;
 * nf4_chunk_kernel<LW, SW> otherwise, with the load form LW = 4 (dword loads: packed
   weight and row stride 4-byte aligned) or 1 (two aligned dwords per chunk joined with
   v_alignbyte: any alignment), and the store form SW = 16 (one 16-byte store per chunk,
@@ -95,6 +96,7 @@ CASES = [
     (6, 4096, 0, 3, 5),
     (1, 600, 0, 0, 9),
     (70, 521, 0, 0, 0),       # rows of 521 (last block of 9): a step crosses a row end in most lanes
+    (9, 4096, 0, 1, 0),       # n % 64 == 0, aligned output, odd packed address (fp32: LW 1, SW 16)
 ]
 
 

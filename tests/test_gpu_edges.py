@@ -37,19 +37,20 @@ pytestmark = pytest.mark.gpu
 FORMS = {
     "dense": (1000, 0, 0, 0, ("bf16", "f16"), "chunk"),              # n % 8 == 0, rows of exactly 4 L bytes
     "dword_whole": (1000, 4, 0, 0, ("bf16", "f32"), "chunk"),        # padded rows: dword loads, 16-byte stores
-    "alignbyte_whole": (1000, 0, 1, 0, ("f16", "f32"), "chunk"),     # odd packed address: dword pairs + v_alignbyte
+    "alignbyte_whole": (1000, 4, 1, 0, ("f16", "f32"), "chunk"),     # odd packed address, padded rows: dword pairs + v_alignbyte
     "dword_staged": (1007, 4, 0, 0, ("bf16", "f16", "f32"), "chunk"),  # padded odd-n rows (stride 508): LDS-staged
     "alignbyte_staged": (1029, 0, 0, 0, ("bf16", "f32"), "chunk"),   # last block of 5 elements, stride 515: both
     "unaligned_out": (1000, 4, 0, 1, ("bf16",), "chunk"),            # padded rows, output one element off: staged
     "short_rows": (200, 0, 0, 0, ("bf16", "f32"), "chunk"),          # L = 25 < 64 chunks: per-step row division
     "short_odd": (77, 0, 0, 0, ("f16",), "chunk"),                   # L = 10, odd n: staged, dword pairs
     "tight_f32": (1007, 0, 0, 0, ("f32",), "chunk"),                 # fp32 of a piece-kernel shape: element stores
-    # the piece kernel (16-bit output, tight rows, n % 8 != 0 or the output off 16 bytes):
+    # the piece kernel (16-bit output, tight rows the dense form does not take):
     "piece_even": (1002, 0, 0, 0, ("bf16", "f16"), "piece"),         # the stream runs on across row ends
     "piece_odd": (1007, 0, 0, 0, ("bf16", "f16"), "piece"),          # a pad nibble at every row end
     "piece_offsets": (1007, 0, 1, 37, ("bf16",), "piece"),           # odd packed address, output 37 elements in
     "piece_aligned_n": (1000, 0, 0, 1, ("f16",), "piece"),           # n % 8 == 0, output one element off
     "piece_min_block": (520, 0, 3, 5, ("bf16",), "piece"),           # last block of 8 elements, rows of 520
+    "piece_unal_packed": (1000, 0, 1, 0, ("f16",), "piece"),         # n % 8 == 0, aligned output, odd packed address
 }
 
 

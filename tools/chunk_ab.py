@@ -12,7 +12,7 @@ launches behind a spin, as bench.py times its steps):
   chunk_4095    4096x4095 (odd n: 2-byte stores)
   chunk_4090    4096x4090 (n % 8 == 2: 4-byte stores)
   pad_4096      4096x4096 with packed rows of 2052 bytes (the general form, dword loads)
-  unal_4096     4096x4096 with the packed weight at an odd address (byte loads)
+  unal_4096     4096x4096 with the packed weight at an odd address (the piece kernel since round 6)
   oal_4096      4096x4096 with the output one element off 16-byte alignment
 --libs a,b: the same cases through other builds of the library (tools/_build/libnf4dq_<x>.so),
 interleaved, tagged "<x>:<case>".
