@@ -81,6 +81,9 @@ constexpr uint32_t kOob = 0x80000000u;  // beyond every buffer range: loads retu
 #ifndef NF4_ABL_X_ON
 #define NF4_ABL_X_ON 1
 #endif
+#ifndef NF4_ABL_XFRAG  // the streaming / persistent body's x fragment (an LDS read)
+#define NF4_ABL_XFRAG(smem_, off_) (*reinterpret_cast<const u32x4*>((smem_) + (off_)))
+#endif
 #ifndef NF4_ABL_SLOAD
 #define NF4_ABL_SLOAD(rsrc_, off_, b8_)                                                       \
     ((b8_) ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8((rsrc_), (off_), 0, 0) \
@@ -1369,7 +1372,7 @@ __device__ __forceinline__ void sslot_mma(const SSlot& s, uint32_t qa, float qb,
         if (st + LA < 8) issue(st + LA);
         u32x4 a[MT];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) a[mt] = *reinterpret_cast<const u32x4*>(smem + xa[mt] + 16u * st);
+        for (int mt = 0; mt < MT; ++mt) a[mt] = NF4_ABL_XFRAG(smem, xa[mt] + 16u * st);
         __builtin_amdgcn_sched_barrier(0);
         uint32_t bw[4];
 #pragma unroll

@@ -50,6 +50,9 @@
 #if defined(ABL_NOX)
 #define NF4_ABL_X_ON 0
 #endif
+#if defined(ABL_NOXR)  // the persistent / streaming body's x fragments from registers (no LDS read; wrong results)
+#define NF4_ABL_XFRAG(smem_, off_) (u32x4{(off_), (off_) ^ 0x3F803F80u, (off_) + 0x3C003C00u, 0x3F803F80u})
+#endif
 #if defined(ABL_NOMMA)
 #define NF4_ABL_MMA_ON 0
 #define NF4_ABL_RED_ON 1
