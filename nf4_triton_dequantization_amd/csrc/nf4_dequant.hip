@@ -1211,6 +1211,149 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
     }
 }
 
+// The piece kernel's fp32 form (quant_state.dtype = torch.float32): a piece is 4 elements,
+// so a wave's step covers 256 elements and its store 1 KiB.  Every tight fp32 shape the flat
+// kernel does not take comes here: the chunk kernel's fp32 stores (two 16-byte halves of a
+// 32-byte chunk per lane, or element stores) write 128-byte lines in pieces from several
+// instructions, 47-58 us for 4096 x 4080..4096 against 13.3 for the flat kernel at 4096^2
+// (profiles/r06/chunk/s17_f32_forms.jsonl).  The per-block tables hold the 16 fp32 products
+// (64 bytes, no rounding); group q holds blocks 2q .. 2q + 3, so a piece's two blocks share a
+// 256-byte group and an element's table address is one v_perm of its code byte (code x 4 in
+// bits 2..5, slot x 64 in bits 6..7).
+constexpr uint32_t kPiece32Tbl = 12 * 256;  // a wave's tables: blocks 0 .. 23 (a wave touches <= 20)
+
+template <int MODE, bool ODD>
+__global__ __launch_bounds__(kWg) void nf4_piece32_kernel(const PieceArgs A) {
+    __shared__ __attribute__((aligned(256))) char ptbl[4 * kPiece32Tbl];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t kw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
+    if (4u * kw >= A.sa + A.elems) return;  // a wave wholly past the end (uniform; no barrier below)
+    const int32_t fw = (int32_t)(4u * kw) - (int32_t)A.sa;  // < 0: wave 0's first pieces
+    const uint32_t fwc = fw < 0 ? 0u : (uint32_t)fw;
+    const uint32_t r0 = fdiv(fwc, A.nf);
+    const uint32_t c0 = fwc - r0 * A.nf.d;
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.prange, kRsrcFlags);
+    int32_t cj[4], bj[4];
+    uint32_t gj[4], aj[4], lo[4], hi[4];
+    {
+        int32_t c = (fw < 0 ? fw : (int32_t)c0) + 4 * (int32_t)lane;
+        uint32_t pb = A.kb + r0 * A.half;
+        uint32_t gb = 0u - (c0 >> 6);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j) c += 256;
+            const bool wrap = c >= (int32_t)A.n;
+            c = wrap ? c - (int32_t)A.n : c;
+            pb = wrap ? pb + A.half : pb;
+            gb = wrap ? gb + A.bpr.d : gb;
+            cj[j] = c;
+            gj[j] = gb;
+            const int32_t b = (int32_t)pb + (c >> 1);
+            bj[j] = b;
+            aj[j] = (uint32_t)(b & ~3);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t a4 = aj[j] + 4u;  // (its own register: see nf4_piece_kernel)
+        asm("" : "+v"(a4));
+        lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, aj[j], 0, 0);
+        hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a4, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t g0 = r0 * A.bpr.d + (c0 >> 6);
+    const uint32_t fl = min((uint32_t)(fw + 1023), A.elems - 1u);
+    const uint32_t rl = fdiv(fl, A.nf);
+    const uint32_t gl = rl * A.bpr.d + ((fl - rl * A.nf.d) >> 6);
+    float sb;
+    {
+        const uint32_t g = min(g0 + lane, gl);
+        const uint32_t r = fdiv(g, A.bpr);
+        const uint32_t b = g - r * A.bpr.d;
+        if constexpr (MODE == kRef) {
+            const float q8 = (float)A.a1[fmodu(g, A.nb)];
+            sb = (q8 / 127.0f) * A.a2[fmodu(opaque_mul(r, A.groups) + (b >> 2), A.n2)];  // IEEE division (:45, :270)
+        } else {
+            sb = A.a2[opaque_mul(r, A.rs) + b];
+        }
+    }
+    const uint32_t region = (threadIdx.x >> 6) * kPiece32Tbl;
+    if (lane < 24u) {
+        // block i: slot i % 2 of group i / 2, and slot i % 2 + 2 of group i / 2 - 1
+        u32x4 e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            e[k] = u32x4{__float_as_uint(__uint_as_float(kNf4Bits[4 * k]) * sb),
+                         __float_as_uint(__uint_as_float(kNf4Bits[4 * k + 1]) * sb),
+                         __float_as_uint(__uint_as_float(kNf4Bits[4 * k + 2]) * sb),
+                         __float_as_uint(__uint_as_float(kNf4Bits[4 * k + 3]) * sb)};  // (:97-98)
+        u32x4_alias* d0 = reinterpret_cast<u32x4_alias*>(ptbl + region + ((lane >> 1) << 8) + ((lane & 1u) << 6));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d0[k] = e[k];
+        if (lane >= 2u) {
+            u32x4_alias* d1 = reinterpret_cast<u32x4_alias*>(ptbl + region + ((lane >> 1) << 8) - 256u + 128u +
+                                                            ((lane & 1u) << 6));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d1[k] = e[k];
+        }
+    }
+    const __amdgpu_buffer_rsrc_t ro =
+        __builtin_amdgcn_make_buffer_rsrc(A.line, 0, 4u * (A.sa + A.elems), kRsrcFlags);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int32_t c = cj[j];
+        const uint32_t cu = (uint32_t)max(c, 0);
+        const uint32_t tA = min(gj[j] + (cu >> 6), 21u);  // (21: lanes past the end)
+        const uint32_t ib = min(min(64u - (cu & 63u), A.n - cu), 4u);
+        // bytes 0 and 1 of E / O: elements 0, 2 / 1, 3; bit 6 of a byte: at or past ib
+        const uint32_t ibr = bytes4(ib);
+        const uint32_t yE = ((0x86848280u - ibr) >> 1) & 0x40404040u;
+        const uint32_t yO = ((0x87858381u - ibr) >> 1) & 0x40404040u;
+        const uint32_t sel = bytes4((uint32_t)bj[j] & 3u) + 0x03020100u;
+        const uint32_t w0 = __builtin_amdgcn_perm(hi[j], lo[j], sel);
+        const uint32_t w1 = __builtin_amdgcn_perm(hi[j], lo[j], sel + 0x01010101u);
+        const uint32_t h0 = __builtin_amdgcn_alignbit(w0, w0, 2u);   // high nibbles x 4 in bits 2..5
+        const uint32_t l0 = __builtin_amdgcn_alignbit(w0, w0, 30u);  // low nibbles x 4
+        const uint32_t h1 = __builtin_amdgcn_alignbit(w1, w1, 2u);
+        const bool odd = (c & 1) != 0;
+        uint32_t E = odd ? l0 : h0, O = odd ? h1 : l0;
+        if constexpr (ODD) {
+            const uint32_t l1 = __builtin_amdgcn_alignbit(w1, w1, 30u);
+            const uint32_t E2 = O, O2 = odd ? l1 : h1;
+            const bool straddle = A.n - cu < 4u;
+            const uint32_t kE = straddle ? yE - (yE >> 4) : 0u;  // 0x3C in the bytes past the end
+            const uint32_t kO = straddle ? yO - (yO >> 4) : 0u;
+            E = (E2 & kE) | (E & ~kE);
+            O = (O2 & kO) | (O & ~kO);
+        }
+        const uint32_t rep = bytes4((tA << 6) & 0x40u);  // slot of block tA in its group, x 64
+        const uint32_t es = (E & 0x3C3C3C3Cu) | (rep + yE);
+        const uint32_t os = (O & 0x3C3C3C3Cu) | (rep + yO);
+        const uint32_t base = region + ((tA >> 1) << 8);
+        uint32_t p[4];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            p[2 * b] = *reinterpret_cast<const uint32_t*>(ptbl + __builtin_amdgcn_perm(es, base, 0x03020104u + b));
+            p[2 * b + 1] = *reinterpret_cast<const uint32_t*>(ptbl + __builtin_amdgcn_perm(os, base, 0x03020104u + b));
+        }
+        const uint32_t k = kw + 64u * (uint32_t)j + lane;
+        const int32_t f = fw + 4 * (64 * j + (int32_t)lane);
+        const bool whole = f >= 0 && (uint32_t)f + 4u <= A.elems;
+        const u32x4 o = {p[0], p[1], p[2], p[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(o, ro, whole ? 16u * k : kDrop, 0, kAuxStore);
+        if (!whole && f < (int32_t)A.elems && f + 4 > 0) {
+            const __amdgpu_buffer_rsrc_t rsp =
+                __builtin_amdgcn_make_buffer_rsrc(A.out, 0, 4u * A.elems, kRsrcFlags);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t oe = 4u * (uint32_t)(f + i);
+                asm("" : "+v"(oe));
+                __builtin_amdgcn_raw_buffer_store_b32(p[i], rsp, oe, 0, kAuxPiece);
+            }
+        }
+    }
+}
+
 // Any length, bitsandbytes semantics: one thread per packed byte.
 struct BnbBytesArgs {
     const uint8_t* packed;
@@ -1450,27 +1593,33 @@ bool dense_eligible(const ChunkArgs& A, int32_t dtype) {
            aligned(A.out, 16) && A.chunks < (1u << 27);
 }
 
-// The piece kernel's shapes: 16-bit outputs of tightly packed rows the dense form does not
-// take (n % 8 != 0, the output off 16-byte alignment, or the packed weight off 4-byte
-// alignment), rows of >= 512 elements whose last block holds >= 8 of them (a piece then
-// touches at most two blocks and a step at most one row end), and offsets below 2^31.
+// The piece kernels' shapes: tightly packed rows the dense form does not take (16-bit output:
+// n % 8 != 0, the output off 16-byte alignment or the packed weight off 4-byte alignment;
+// fp32: every such shape), rows of >= 512 elements whose last block holds >= 8 of them (a
+// piece then touches at most two blocks and a step at most one row end), and offsets below 2^31.
 bool piece_eligible(const ChunkArgs& A, int32_t dtype) {
     const uint64_t half = (A.n + 1u) / 2u;
     const uint64_t rows = A.out_elems / A.n;
-    return dtype != NF4DQ_F32 && A.stride == half &&
-           A.packed_len == rows * half && A.n >= 512u && (A.n % 64u == 0 || A.n % 64u >= 8u) &&
-           2u * (A.out_elems + 64u) < (uint64_t(1) << 31) && A.packed_len + 8u < (uint64_t(1) << 31);
+    const uint64_t ob = dtype == NF4DQ_F32 ? 4u : 2u;
+    return A.stride == half && A.packed_len == rows * half && A.n >= 512u && (A.n % 64u == 0 || A.n % 64u >= 8u) &&
+           ob * (A.out_elems + 64u) < (uint64_t(1) << 31) && A.packed_len + 8u < (uint64_t(1) << 31);
 }
 
 template <int MODE, int DT>
 void launch_pieces_dt(const PieceArgs& P, unsigned g, hipStream_t st) {
-    if (P.n & 1u) hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, true>), dim3(g), dim3(kWg), 0, st, P);
-    else hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, false>), dim3(g), dim3(kWg), 0, st, P);
+    if constexpr (DT == NF4DQ_F32) {
+        if (P.n & 1u) hipLaunchKernelGGL((nf4_piece32_kernel<MODE, true>), dim3(g), dim3(kWg), 0, st, P);
+        else hipLaunchKernelGGL((nf4_piece32_kernel<MODE, false>), dim3(g), dim3(kWg), 0, st, P);
+    } else {
+        if (P.n & 1u) hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, true>), dim3(g), dim3(kWg), 0, st, P);
+        else hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, false>), dim3(g), dim3(kWg), 0, st, P);
+    }
 }
 
 template <int MODE>
 int launch_pieces(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
     PieceArgs P{};
+    const uint32_t ob = dtype == NF4DQ_F32 ? 4u : 2u, per = 16u / ob;  // output bytes, elements per piece
     const uintptr_t pw = (uintptr_t)A.packed, ow = (uintptr_t)A.out;
     P.packed = reinterpret_cast<const uint8_t*>(pw & ~uintptr_t(3));
     P.kb = (uint32_t)(pw & 3u);
@@ -1479,7 +1628,7 @@ int launch_pieces(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
     P.a2 = A.a2;
     P.out = A.out;
     P.line = reinterpret_cast<void*>(ow & ~uintptr_t(127));
-    P.sa = (uint32_t)((ow & 127u) / 2u);
+    P.sa = (uint32_t)((ow & 127u) / ob);
     P.elems = (uint32_t)A.out_elems;
     P.n = A.n;
     P.half = (A.n + 1u) / 2u;
@@ -1489,10 +1638,11 @@ int launch_pieces(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
     P.nb = A.nb;
     P.n2 = A.n2;
     P.rs = A.rs;
-    const uint32_t pieces = (P.sa + P.elems + 7u) / 8u;
+    const uint32_t pieces = (P.sa + P.elems + per - 1u) / per;
     const unsigned g = (pieces + 1023u) / 1024u;  // 4 waves x 256 pieces
     if (dtype == NF4DQ_BF16) launch_pieces_dt<MODE, NF4DQ_BF16>(P, g, st);
-    else launch_pieces_dt<MODE, NF4DQ_F16>(P, g, st);
+    else if (dtype == NF4DQ_F16) launch_pieces_dt<MODE, NF4DQ_F16>(P, g, st);
+    else launch_pieces_dt<MODE, NF4DQ_F32>(P, g, st);
     return hip_rc(hipGetLastError());
 }
 

@@ -8,7 +8,8 @@ class of shape on purpose, for every load / store form of the chunk kernels
 (csrc/nf4_dequant.hip: the dense form; the general form with dword loads or alignbyte
 dword pairs, whole-chunk 16-byte stores or LDS staging, rows of >= 64 chunks or fewer)
 and of the piece kernel (16-bit outputs of tight rows in output order: even and odd n,
-odd packed and output offsets, the shortest last block it takes), in both scale modes:
+odd packed and output offsets, the shortest last block it takes; its fp32 form), in both
+scale modes:
 
 * m is chosen so that the last workgroup (4 waves x 256 four-byte chunks, or 256 16-byte
   output pieces) holds 1, 2 and 3 waves wholly past the end, and 0 as the control;
@@ -43,7 +44,6 @@ FORMS = {
     "unaligned_out": (1000, 4, 0, 1, ("bf16",), "chunk"),            # padded rows, output one element off: staged
     "short_rows": (200, 0, 0, 0, ("bf16", "f32"), "chunk"),          # L = 25 < 64 chunks: per-step row division
     "short_odd": (77, 0, 0, 0, ("f16",), "chunk"),                   # L = 10, odd n: staged, dword pairs
-    "tight_f32": (1007, 0, 0, 0, ("f32",), "chunk"),                 # fp32 of a piece-kernel shape: element stores
     # the piece kernel (16-bit output, tight rows the dense form does not take):
     "piece_even": (1002, 0, 0, 0, ("bf16", "f16"), "piece"),         # the stream runs on across row ends
     "piece_odd": (1007, 0, 0, 0, ("bf16", "f16"), "piece"),          # a pad nibble at every row end
@@ -51,6 +51,10 @@ FORMS = {
     "piece_aligned_n": (1000, 0, 0, 1, ("f16",), "piece"),           # n % 8 == 0, output one element off
     "piece_min_block": (520, 0, 3, 5, ("bf16",), "piece"),           # last block of 8 elements, rows of 520
     "piece_unal_packed": (1000, 0, 1, 0, ("f16",), "piece"),         # n % 8 == 0, aligned output, odd packed address
+    # its fp32 form (4-element pieces; every tight fp32 shape the flat kernel does not take)
+    "piece32_odd": (1007, 0, 1, 5, ("f32",), "piece32"),
+    "piece32_even": (1002, 0, 0, 0, ("f32",), "piece32"),
+    "piece32_aligned_n": (1000, 0, 0, 0, ("f32",), "piece32"),       # n % 8 == 0, everything aligned
 }
 
 
@@ -60,10 +64,14 @@ def _chunks_per_row(n):
 
 def _units(form, m):
     """256 of these per wave: 4-byte packed chunks (chunk kernels) or 16-byte output pieces
-    from the output's 128-byte line (the piece kernel; torch allocations are 128-aligned and
-    the sentinel is 64 elements, so the output sits `ooff` elements into its line)."""
+    from the output's 128-byte line (the piece kernels; torch allocations are 128-aligned and
+    the sentinel is 64 elements, so the output sits `ooff` elements into its line, modulo the
+    line's 64 16-bit / 32 fp32 elements)."""
     n, _, _, ooff, _, kind = FORMS[form]
-    return m * _chunks_per_row(n) if kind == "chunk" else -(-(ooff + m * n) // 8)
+    if kind == "chunk":
+        return m * _chunks_per_row(n)
+    per = 8 if kind == "piece" else 4  # elements per 16-byte piece
+    return -(-(ooff % (128 // (16 // per)) + m * n) // per)
 
 
 def _m_with_past_end_waves(form, k, m0=1):

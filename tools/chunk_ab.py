@@ -14,6 +14,7 @@ launches behind a spin, as bench.py times its steps):
   pad_4096      4096x4096 with packed rows of 2052 bytes (the general form, dword loads)
   unal_4096     4096x4096 with the packed weight at an odd address (the piece kernel since round 6)
   oal_4096      4096x4096 with the output one element off 16-byte alignment
+--dtype f32 / f16: the output type (default bf16).
 --libs a,b: the same cases through other builds of the library (tools/_build/libnf4dq_<x>.so),
 interleaved, tagged "<x>:<case>".
 Prints one JSON line per case: median / min / max us per launch and the fraction of
@@ -51,12 +52,16 @@ def case_key(name):
     return (m, n, PAD.get(name, 0), UNAL.get(name, 0), OOFF.get(name, 0))
 
 
+TDT = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32}
+DT = TDT["bf16"]  # (set by --dtype)
+
+
 def case_sets(name, dev, gen):
     """(input sets, output sets) of a case, rotated as bench.py rotates (>= 512 MiB of
     distinct reads and of writes: HBM-streamed)."""
     m, n, _ = SHAPES[name]
     key = case_key(name)
-    pin, pout = rotation(m, n, 2)
+    pin, pout = rotation(m, n, DT.itemsize)
     if n % 2 or key[2] or key[3] or key[4]:  # packed rows of ceil(n/2) + pad bytes, at byte offset unal
         ins = []
         stride = (n + 1) // 2 + key[2]
@@ -66,9 +71,9 @@ def case_sets(name, dev, gen):
             ins.append((q[key[3]:],
                         torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen),
                         torch.rand((nb + 255) // 256, device=dev, generator=gen) * 0.01 + 1e-3))
-        outs = [torch.empty((m * n + 64,), dtype=torch.bfloat16, device=dev)[key[4]:] for _ in range(pout)]
+        outs = [torch.empty((m * n + 64,), dtype=DT, device=dev)[key[4]:] for _ in range(pout)]
         return ins, outs
-    return rotating_sets(m, n, torch.bfloat16, dev, gen, pin, pout)
+    return rotating_sets(m, n, DT, dev, gen, pin, pout)
 
 
 def main():
@@ -77,7 +82,11 @@ def main():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--cases", default="flat_4096,chunk_4096,chunk_4080,rows_4080,chunk_4095,chunk_4090")
     ap.add_argument("--libs", default="")
+    ap.add_argument("--dtype", default="bf16", choices=sorted(TDT))
     args = ap.parse_args()
+    global DT
+    DT = TDT[args.dtype]
+    dcode = {"bf16": _lib.BF16, "f16": _lib.F16, "f32": _lib.F32}[args.dtype]
     dev = torch.device("cuda", 0)
     libs = {"prod": _lib.lib()}
     for path in [v for v in args.libs.split(",") if v]:
@@ -114,11 +123,11 @@ def main():
             o = outs[i % len(outs)]
             if flags:
                 rc = L.nf4_dequant_ref_cfg(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(),
-                                           a2.numel(), o.data_ptr(), _lib.BF16, m, n, ctypes.byref(cfgs[flags]),
+                                           a2.numel(), o.data_ptr(), dcode, m, n, ctypes.byref(cfgs[flags]),
                                            st.cuda_stream)
             else:
                 rc = L.nf4_dequant_ref(q.data_ptr(), q.numel(), a1.data_ptr(), a1.numel(), a2.data_ptr(), a2.numel(),
-                                       o.data_ptr(), _lib.BF16, m, n, st.cuda_stream)
+                                       o.data_ptr(), dcode, m, n, st.cuda_stream)
             assert rc == 0, rc
         return launch
 
@@ -146,8 +155,8 @@ def main():
         m, n, flags = SHAPES[nm.split(":")[1]]
         ts = sorted(res[nm])
         med = ts[len(ts) // 2]
-        byt = alg_bytes(m, n, 2)
-        print(json.dumps({"case": nm, "m": m, "n": n, "flags": flags, "steps": args.steps, "rounds": args.rounds,
+        byt = alg_bytes(m, n, DT.itemsize)
+        print(json.dumps({"case": nm, "m": m, "n": n, "dtype": args.dtype, "flags": flags, "steps": args.steps, "rounds": args.rounds,
                           "us_median": round(med, 3), "us_min": round(ts[0], 3), "us_max": round(ts[-1], 3),
                           "frac": round(byt / (med * 1e-6) / PEAK, 4)}), flush=True)
 
