@@ -25,6 +25,10 @@
 //   DQV_LD64=1 the piece kernel's 8-byte packed loads (NF4_DQ_PIECE_LD64): 5-13 % slower in
 //              round 6 (profiles/r06/chunk/s14_piece_ld64_ab.jsonl); the hook removed after
 //              measurement (in git history at the commit that adds that file)
+//   DQV_F32ST=p  cache-policy bits of the chunk kernel's fp32 half-chunk stores (padded rows):
+//              0 (default policy) 18.3 us at padded 4096^2 fp32 against 57.2 (sc1 + nt) and 41.5
+//              (sc1), round 6 (profiles/r06/chunk/s19_f32_half_store_policy.jsonl); 0 is now the
+//              product's and the hook is gone
 //   DQV_DEC=n  16-bit output decode (NF4_DQ_DECODE: 0 per-nibble lookup + multiply, 1 per-block LDS table)
 #ifdef DQV_WG
 #define NF4_DQ_FLAT_WAVES DQV_WG
