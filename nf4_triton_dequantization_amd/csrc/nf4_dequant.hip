@@ -1060,41 +1060,46 @@ constexpr uint32_t kPieceTbl = 4096;  // a wave's tables: 16 groups x 8 blocks x
 // v_mul_lo_u32, and the constant does not fit v_mul_u32_u24's 24 bits)
 __device__ __forceinline__ uint32_t bytes4(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0u); }
 
-template <int DT, int MODE, bool ODD>
-__global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
-    __shared__ __attribute__((aligned(256))) char ptbl[4 * kPieceTbl];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t kw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
-    if (8u * kw >= A.sa + A.elems) return;  // a wave wholly past the end (uniform; no barrier below)
-    // the wave's first element (< 0: wave 0, whose first pieces start before the output)
-    const int32_t fw = (int32_t)(8u * kw) - (int32_t)A.sa;
-    const uint32_t fwc = fw < 0 ? 0u : (uint32_t)fw;
+// One wave of a piece kernel (EP elements per 16-byte piece, 4 steps of 64 pieces): each
+// step's column (of the piece's first element; < 0 before the output: wave 0's first
+// pieces), its row's first block from g0, and the two packed dwords around its nibbles --
+// all loads out first.  A step moves 64 EP <= 512 elements and rows are >= 512: at most one
+// row end per step, so every index advances by additions.  false: the wave lies wholly
+// past the end (it must return; no barrier follows in either kernel).
+template <uint32_t EP>
+struct PieceWave {
+    int32_t fw;              // the wave's first element (< 0: wave 0)
+    uint32_t c0, g0, gl;     // column of its first element in the matrix; its first / last block
+    int32_t c[4], b[4];      // per step: column, byte of nibble c from `packed`
+    uint32_t gr[4], lo[4], hi[4];  // per step: the row's first block from g0; the two dwords
+};
+
+template <uint32_t EP>
+__device__ __forceinline__ bool piece_wave(const PieceArgs& A, uint32_t kw, uint32_t lane, PieceWave<EP>& W) {
+    if (EP * kw >= A.sa + A.elems) return false;
+    W.fw = (int32_t)(EP * kw) - (int32_t)A.sa;
+    const uint32_t fwc = W.fw < 0 ? 0u : (uint32_t)W.fw;
     const uint32_t r0 = fdiv(fwc, A.nf);
-    const uint32_t c0 = fwc - r0 * A.nf.d;
+    W.c0 = fwc - r0 * A.nf.d;
     const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.prange, kRsrcFlags);
-    // Each step's column (of the piece's first element; < 0 before the output) and rows
-    // past r0 (a step moves 512 elements, rows are >= 512: at most one row end per step),
-    // then the two dwords around the piece's nibbles -- all loads out first.
-    int32_t cj[4], bj[4];
-    uint32_t gj[4], aj[4], lo[4], hi[4];
+    uint32_t aj[4];
     {
-        int32_t c = (fw < 0 ? fw : (int32_t)c0) + 8 * (int32_t)lane;
+        int32_t c = (W.fw < 0 ? W.fw : (int32_t)W.c0) + (int32_t)(EP * lane);
         uint32_t pb = A.kb + r0 * A.half;  // the row's first packed byte, from `packed`
-        uint32_t gb = 0u - (c0 >> 6);       // the row's first block, from g0 (below)
+        uint32_t gb = 0u - (W.c0 >> 6);     // the row's first block, from g0
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (j) c += 512;
+            if (j) c += (int32_t)(64u * EP);
             const bool wrap = c >= (int32_t)A.n;  // (additions only: no multiply per step)
             c = wrap ? c - (int32_t)A.n : c;
             pb = wrap ? pb + A.half : pb;
             gb = wrap ? gb + A.bpr.d : gb;
-            cj[j] = c;
-            gj[j] = gb;
+            W.c[j] = c;
+            W.gr[j] = gb;
             // the byte holding nibble c of the row (before the weight: negative, i.e. beyond
             // the range once unsigned -- the load returns 0)
-            const int32_t b = (int32_t)pb + (c >> 1);
-            bj[j] = b;
-            aj[j] = (uint32_t)(b & ~3);
+            W.b[j] = (int32_t)pb + (c >> 1);
+            aj[j] = (uint32_t)(W.b[j] & ~3);
         }
     }
 #pragma unroll
@@ -1106,27 +1111,76 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
         // 5-13 % slower, round 6 s14.)
         uint32_t a4 = aj[j] + 4u;
         asm("" : "+v"(a4));
-        lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, aj[j], 0, 0);
-        hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a4, 0, 0);
+        W.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, aj[j], 0, 0);
+        W.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a4, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    // The wave's blocks are consecutive and at most 38: lane i rounds block g0 + i's table.
-    const uint32_t g0 = r0 * A.bpr.d + (c0 >> 6);
-    const uint32_t fl = min((uint32_t)(fw + 2047), A.elems - 1u);
+    W.g0 = r0 * A.bpr.d + (W.c0 >> 6);
+    const uint32_t fl = min((uint32_t)(W.fw + (int32_t)(256u * EP) - 1), A.elems - 1u);
     const uint32_t rl = fdiv(fl, A.nf);
-    const uint32_t gl = rl * A.bpr.d + ((fl - rl * A.nf.d) >> 6);
-    float sb;
-    {
-        const uint32_t g = min(g0 + lane, gl);
-        const uint32_t r = fdiv(g, A.bpr);
-        const uint32_t b = g - r * A.bpr.d;
-        if constexpr (MODE == kRef) {
-            const float q8 = (float)A.a1[fmodu(g, A.nb)];
-            sb = (q8 / 127.0f) * A.a2[fmodu(opaque_mul(r, A.groups) + (b >> 2), A.n2)];  // IEEE division (:45, :270)
-        } else {
-            sb = A.a2[opaque_mul(r, A.rs) + b];
-        }
+    W.gl = rl * A.bpr.d + ((fl - rl * A.nf.d) >> 6);
+    return true;
+}
+
+// The scale of block min(g0 + lane, gl) (the wave's blocks are consecutive; lane i rounds
+// block g0 + i's table).
+template <int MODE>
+__device__ __forceinline__ float piece_scale(const PieceArgs& A, uint32_t g0, uint32_t gl, uint32_t lane) {
+    const uint32_t g = min(g0 + lane, gl);
+    const uint32_t r = fdiv(g, A.bpr);
+    const uint32_t b = g - r * A.bpr.d;
+    if constexpr (MODE == kRef) {
+        const float q8 = (float)A.a1[fmodu(g, A.nb)];
+        return (q8 / 127.0f) * A.a2[fmodu(opaque_mul(r, A.groups) + (b >> 2), A.n2)];  // IEEE division (:45, :270)
+    } else {
+        return A.a2[opaque_mul(r, A.rs) + b];
     }
+}
+
+// A piece's table-address bytes: es byte i for element 2i, os byte i for element 2i + 1, each
+// the element's code << SH (SH = log2 of the table entry's bytes: 1 for 16-bit, 2 for fp32)
+// ORed with its block's slot in the group << (SH + 4): `slot` for the piece's first block,
+// slot + 1 from element ib on.  Nibble c of a row is the high nibble of its byte when c is
+// even; W0 = bytes b .. b+3, W1 = b+1 .. b+4 of the two loaded dwords.  ODD (odd n): the
+// elements past the row's end (a straddling piece) sit one nibble further on (the pad).
+template <int SH, bool ODD>
+__device__ __forceinline__ void piece_codes(uint32_t lo, uint32_t hi, int32_t b, int32_t c, uint32_t ib,
+                                            bool straddle, uint32_t slot, uint32_t& es, uint32_t& os) {
+    constexpr uint32_t kCode = 0x0F0F0F0Fu << SH, kStep = 0x01010101u << (SH + 4);
+    // bit SH + 4 of each byte of yE / yO: the element lies at or past ib (0x80 + 2i - ib >=
+    // 0x80, bytes never borrow)
+    const uint32_t ibr = bytes4(ib);
+    const uint32_t yE = ((0x86848280u - ibr) >> (3 - SH)) & kStep;
+    const uint32_t yO = ((0x87858381u - ibr) >> (3 - SH)) & kStep;
+    const uint32_t sel = bytes4((uint32_t)b & 3u) + 0x03020100u;
+    const uint32_t w0 = __builtin_amdgcn_perm(hi, lo, sel);
+    const uint32_t w1 = __builtin_amdgcn_perm(hi, lo, sel + 0x01010101u);
+    const uint32_t h0 = __builtin_amdgcn_alignbit(w0, w0, 4u - SH);   // high nibbles << SH
+    const uint32_t l0 = __builtin_amdgcn_alignbit(w0, w0, 32u - SH);  // low nibbles << SH
+    const uint32_t h1 = __builtin_amdgcn_alignbit(w1, w1, 4u - SH);
+    const bool odd = (c & 1) != 0;
+    uint32_t E = odd ? l0 : h0, O = odd ? h1 : l0;
+    if constexpr (ODD) {
+        const uint32_t l1 = __builtin_amdgcn_alignbit(w1, w1, 32u - SH);
+        const uint32_t E2 = O, O2 = odd ? l1 : h1;
+        const uint32_t kE = straddle ? yE - (yE >> 4) : 0u;  // the code bits of the bytes past the end
+        const uint32_t kO = straddle ? yO - (yO >> 4) : 0u;
+        E = (E2 & kE) | (E & ~kE);
+        O = (O2 & kO) | (O & ~kO);
+    }
+    const uint32_t rep = bytes4(slot << (SH + 4));
+    es = (E & kCode) | (rep + yE);
+    os = (O & kCode) | (rep + yO);
+}
+
+template <int DT, int MODE, bool ODD>
+__global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
+    __shared__ __attribute__((aligned(256))) char ptbl[4 * kPieceTbl];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t kw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
+    PieceWave<8> W;
+    if (!piece_wave<8>(A, kw, lane, W)) return;  // (uniform)
+    const float sb = piece_scale<MODE>(A, W.g0, W.gl, lane);
     const uint32_t region = (threadIdx.x >> 6) * kPieceTbl;
     {
         uint32_t e[8];
@@ -1148,54 +1202,25 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
         __builtin_amdgcn_make_buffer_rsrc(A.line, 0, 2u * (A.sa + A.elems), kRsrcFlags);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int32_t c = cj[j];
         // (c < 0: wave 0's first pieces, whose elements are block 0's or dropped)
-        const uint32_t cu = (uint32_t)max(c, 0);
+        const uint32_t cu = (uint32_t)max(W.c[j], 0);
         // the piece's first block (from g0) and the first element of the next block, if any
         // (8: none): a boundary inside the row or the row's end, whichever comes first --
         // the row end, when inside the piece, is the first (the last block holds >= 8)
-        const uint32_t tA = min(gj[j] + (cu >> 6), 59u);  // (59: lanes past the end)
+        const uint32_t tA = min(W.gr[j] + (cu >> 6), 59u);  // (59: lanes past the end)
         const uint32_t ib = min(min(64u - (cu & 63u), A.n - cu), 8u);
-        // byte i of E is element 2i, of O element 2i + 1; bit 5 of each byte of yE / yO: the
-        // element lies at or past ib (0x80 + 2i - ib >= 0x80, bytes never borrow)
-        const uint32_t ibr = bytes4(ib);
-        const uint32_t yE = ((0x86848280u - ibr) >> 2) & 0x20202020u;
-        const uint32_t yO = ((0x87858381u - ibr) >> 2) & 0x20202020u;
-        // elements 2i (E) and 2i + 1 (O) as code bytes: nibble c of the row is the high
-        // nibble of its byte when c is even.  W0 = bytes b .. b+3, W1 = b+1 .. b+4.
-        const uint32_t sel = bytes4((uint32_t)bj[j] & 3u) + 0x03020100u;
-        const uint32_t w0 = __builtin_amdgcn_perm(hi[j], lo[j], sel);
-        const uint32_t w1 = __builtin_amdgcn_perm(hi[j], lo[j], sel + 0x01010101u);
-        const uint32_t h0 = __builtin_amdgcn_alignbit(w0, w0, 3u);   // high nibbles x 2 in bits 1..4
-        const uint32_t l0 = __builtin_amdgcn_alignbit(w0, w0, 31u);  // low nibbles x 2
-        const uint32_t h1 = __builtin_amdgcn_alignbit(w1, w1, 3u);
-        const bool odd = (c & 1) != 0;
-        uint32_t E = odd ? l0 : h0, O = odd ? h1 : l0;
-        if constexpr (ODD) {
-            // odd n: the elements past the row's end sit one nibble further on (the pad)
-            const uint32_t l1 = __builtin_amdgcn_alignbit(w1, w1, 31u);
-            const uint32_t E2 = O, O2 = odd ? l1 : h1;
-            const bool straddle = A.n - cu < 8u;
-            const uint32_t kE = straddle ? yE - (yE >> 4) : 0u;  // 0x1E in the bytes past the end
-            const uint32_t kO = straddle ? yO - (yO >> 4) : 0u;
-            E = (E2 & kE) | (E & ~kE);
-            O = (O2 & kO) | (O & ~kO);
-        }
-        const uint32_t rep = bytes4((tA << 5) & 0x60u);  // slot of block tA in its group, x 32
-        const uint32_t es = (E & 0x1E1E1E1Eu) | (rep + yE);
-        const uint32_t os = (O & 0x1E1E1E1Eu) | (rep + yO);
+        uint32_t es, os;
+        piece_codes<1, ODD>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib, A.n - cu < 8u, tA & 3u, es, os);
         const uint32_t base = region + ((tA >> 2) << 8);
         uint32_t p[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const uint32_t ae = __builtin_amdgcn_perm(es, base, 0x03020104u + b);
-            const uint32_t ao = __builtin_amdgcn_perm(os, base, 0x03020104u + b);
-            const uint32_t ve = *reinterpret_cast<const u16_alias*>(ptbl + ae);
-            const uint32_t vo = *reinterpret_cast<const u16_alias*>(ptbl + ao);
+            const uint32_t ve = *reinterpret_cast<const u16_alias*>(ptbl + __builtin_amdgcn_perm(es, base, 0x03020104u + b));
+            const uint32_t vo = *reinterpret_cast<const u16_alias*>(ptbl + __builtin_amdgcn_perm(os, base, 0x03020104u + b));
             p[b] = __builtin_amdgcn_perm(vo, ve, 0x05040100u);  // (one v_perm; the compiler made shift + or_sdwa)
         }
         const uint32_t k = kw + 64u * (uint32_t)j + lane;
-        const int32_t f = fw + 8 * (64 * j + (int32_t)lane);
+        const int32_t f = W.fw + 8 * (64 * j + (int32_t)lane);
         const bool whole = f >= 0 && (uint32_t)f + 8u <= A.elems;
         const u32x4 o = {p[0], p[1], p[2], p[3]};
         __builtin_amdgcn_raw_buffer_store_b128(o, ro, whole ? 16u * k : kDrop, 0, kAuxStore);
@@ -1207,7 +1232,7 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 uint32_t oe = 2u * (uint32_t)(f + i);
-                asm("" : "+v"(oe));  // (each offset its own register: see a4 above)
+                asm("" : "+v"(oe));  // (each offset its own register: see piece_wave)
                 __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(p[i >> 1] >> (16 * (i & 1))), rsp, oe, 0,
                                                       kAuxPiece);
             }
@@ -1231,56 +1256,9 @@ __global__ __launch_bounds__(kWg) void nf4_piece32_kernel(const PieceArgs A) {
     __shared__ __attribute__((aligned(256))) char ptbl[4 * kPiece32Tbl];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t kw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
-    if (4u * kw >= A.sa + A.elems) return;  // a wave wholly past the end (uniform; no barrier below)
-    const int32_t fw = (int32_t)(4u * kw) - (int32_t)A.sa;  // < 0: wave 0's first pieces
-    const uint32_t fwc = fw < 0 ? 0u : (uint32_t)fw;
-    const uint32_t r0 = fdiv(fwc, A.nf);
-    const uint32_t c0 = fwc - r0 * A.nf.d;
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.prange, kRsrcFlags);
-    int32_t cj[4], bj[4];
-    uint32_t gj[4], aj[4], lo[4], hi[4];
-    {
-        int32_t c = (fw < 0 ? fw : (int32_t)c0) + 4 * (int32_t)lane;
-        uint32_t pb = A.kb + r0 * A.half;
-        uint32_t gb = 0u - (c0 >> 6);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (j) c += 256;
-            const bool wrap = c >= (int32_t)A.n;
-            c = wrap ? c - (int32_t)A.n : c;
-            pb = wrap ? pb + A.half : pb;
-            gb = wrap ? gb + A.bpr.d : gb;
-            cj[j] = c;
-            gj[j] = gb;
-            const int32_t b = (int32_t)pb + (c >> 1);
-            bj[j] = b;
-            aj[j] = (uint32_t)(b & ~3);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        uint32_t a4 = aj[j] + 4u;  // (its own register: see nf4_piece_kernel)
-        asm("" : "+v"(a4));
-        lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, aj[j], 0, 0);
-        hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a4, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const uint32_t g0 = r0 * A.bpr.d + (c0 >> 6);
-    const uint32_t fl = min((uint32_t)(fw + 1023), A.elems - 1u);
-    const uint32_t rl = fdiv(fl, A.nf);
-    const uint32_t gl = rl * A.bpr.d + ((fl - rl * A.nf.d) >> 6);
-    float sb;
-    {
-        const uint32_t g = min(g0 + lane, gl);
-        const uint32_t r = fdiv(g, A.bpr);
-        const uint32_t b = g - r * A.bpr.d;
-        if constexpr (MODE == kRef) {
-            const float q8 = (float)A.a1[fmodu(g, A.nb)];
-            sb = (q8 / 127.0f) * A.a2[fmodu(opaque_mul(r, A.groups) + (b >> 2), A.n2)];  // IEEE division (:45, :270)
-        } else {
-            sb = A.a2[opaque_mul(r, A.rs) + b];
-        }
-    }
+    PieceWave<4> W;
+    if (!piece_wave<4>(A, kw, lane, W)) return;  // (uniform)
+    const float sb = piece_scale<MODE>(A, W.g0, W.gl, lane);
     const uint32_t region = (threadIdx.x >> 6) * kPiece32Tbl;
     if (lane < 24u) {
         // block i: slot i % 2 of group i / 2, and slot i % 2 + 2 of group i / 2 - 1
@@ -1305,34 +1283,11 @@ __global__ __launch_bounds__(kWg) void nf4_piece32_kernel(const PieceArgs A) {
         __builtin_amdgcn_make_buffer_rsrc(A.line, 0, 4u * (A.sa + A.elems), kRsrcFlags);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int32_t c = cj[j];
-        const uint32_t cu = (uint32_t)max(c, 0);
-        const uint32_t tA = min(gj[j] + (cu >> 6), 21u);  // (21: lanes past the end)
+        const uint32_t cu = (uint32_t)max(W.c[j], 0);
+        const uint32_t tA = min(W.gr[j] + (cu >> 6), 21u);  // (21: lanes past the end)
         const uint32_t ib = min(min(64u - (cu & 63u), A.n - cu), 4u);
-        // bytes 0 and 1 of E / O: elements 0, 2 / 1, 3; bit 6 of a byte: at or past ib
-        const uint32_t ibr = bytes4(ib);
-        const uint32_t yE = ((0x86848280u - ibr) >> 1) & 0x40404040u;
-        const uint32_t yO = ((0x87858381u - ibr) >> 1) & 0x40404040u;
-        const uint32_t sel = bytes4((uint32_t)bj[j] & 3u) + 0x03020100u;
-        const uint32_t w0 = __builtin_amdgcn_perm(hi[j], lo[j], sel);
-        const uint32_t w1 = __builtin_amdgcn_perm(hi[j], lo[j], sel + 0x01010101u);
-        const uint32_t h0 = __builtin_amdgcn_alignbit(w0, w0, 2u);   // high nibbles x 4 in bits 2..5
-        const uint32_t l0 = __builtin_amdgcn_alignbit(w0, w0, 30u);  // low nibbles x 4
-        const uint32_t h1 = __builtin_amdgcn_alignbit(w1, w1, 2u);
-        const bool odd = (c & 1) != 0;
-        uint32_t E = odd ? l0 : h0, O = odd ? h1 : l0;
-        if constexpr (ODD) {
-            const uint32_t l1 = __builtin_amdgcn_alignbit(w1, w1, 30u);
-            const uint32_t E2 = O, O2 = odd ? l1 : h1;
-            const bool straddle = A.n - cu < 4u;
-            const uint32_t kE = straddle ? yE - (yE >> 4) : 0u;  // 0x3C in the bytes past the end
-            const uint32_t kO = straddle ? yO - (yO >> 4) : 0u;
-            E = (E2 & kE) | (E & ~kE);
-            O = (O2 & kO) | (O & ~kO);
-        }
-        const uint32_t rep = bytes4((tA << 6) & 0x40u);  // slot of block tA in its group, x 64
-        const uint32_t es = (E & 0x3C3C3C3Cu) | (rep + yE);
-        const uint32_t os = (O & 0x3C3C3C3Cu) | (rep + yO);
+        uint32_t es, os;
+        piece_codes<2, ODD>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib, A.n - cu < 4u, tA & 1u, es, os);
         const uint32_t base = region + ((tA >> 1) << 8);
         uint32_t p[4];
 #pragma unroll
@@ -1341,7 +1296,7 @@ __global__ __launch_bounds__(kWg) void nf4_piece32_kernel(const PieceArgs A) {
             p[2 * b + 1] = *reinterpret_cast<const uint32_t*>(ptbl + __builtin_amdgcn_perm(os, base, 0x03020104u + b));
         }
         const uint32_t k = kw + 64u * (uint32_t)j + lane;
-        const int32_t f = fw + 4 * (64 * j + (int32_t)lane);
+        const int32_t f = W.fw + 4 * (64 * j + (int32_t)lane);
         const bool whole = f >= 0 && (uint32_t)f + 4u <= A.elems;
         const u32x4 o = {p[0], p[1], p[2], p[3]};
         __builtin_amdgcn_raw_buffer_store_b128(o, ro, whole ? 16u * k : kDrop, 0, kAuxStore);
