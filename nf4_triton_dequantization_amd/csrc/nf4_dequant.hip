@@ -1032,11 +1032,11 @@ __global__ __launch_bounds__(kWg) void nf4_chunk_kernel(const ChunkArgs A) {
 // pad nibble), so a piece starts at any nibble; the lane loads the two dwords around its
 // 5 bytes and forms the even and odd elements' code bytes with byte permutes and
 // rotates.  A piece can hold two scale blocks (a block boundary inside the row, or the
-// row's end: the next row's first block is the next block; rows whose last block is
-// shorter than 8 elements are left to the chunk kernel).  The per-block tables of 16
-// rounded outputs (as in the dense form) sit in 16 OVERLAPPING groups of 8 blocks --
-// group q holds blocks 4q .. 4q + 7 -- so both blocks of a piece lie in group tA / 4 and
-// one v_perm per element still forms its table address.
+// row's end: the next row's first block is the next block), three when a row's last block
+// is shorter than a piece.  The per-block tables of 16 rounded outputs (as in the dense
+// form) sit in 16 OVERLAPPING groups of 8 blocks -- group q holds blocks 4q .. 4q + 7 -- so
+// the blocks of a piece lie in group tA / 4 and one v_perm per element still forms its
+// table address.
 struct PieceArgs {
     const uint8_t* packed;  // the packed weight aligned down to 4 bytes
     const uint8_t* a1;
@@ -1139,19 +1139,34 @@ __device__ __forceinline__ float piece_scale(const PieceArgs& A, uint32_t g0, ui
 
 // A piece's table-address bytes: es byte i for element 2i, os byte i for element 2i + 1, each
 // the element's code << SH (SH = log2 of the table entry's bytes: 1 for 16-bit, 2 for fp32)
-// ORed with its block's slot in the group << (SH + 4): `slot` for the piece's first block,
-// slot + 1 from element ib on.  Nibble c of a row is the high nibble of its byte when c is
-// even; W0 = bytes b .. b+3, W1 = b+1 .. b+4 of the two loaded dwords.  ODD (odd n): the
-// elements past the row's end (a straddling piece) sit one nibble further on (the pad).
-template <int SH, bool ODD>
-__device__ __forceinline__ void piece_codes(uint32_t lo, uint32_t hi, int32_t b, int32_t c, uint32_t ib,
-                                            bool straddle, uint32_t slot, uint32_t& es, uint32_t& os) {
-    constexpr uint32_t kCode = 0x0F0F0F0Fu << SH, kStep = 0x01010101u << (SH + 4);
-    // bit SH + 4 of each byte of yE / yO: the element lies at or past ib (0x80 + 2i - ib >=
-    // 0x80, bytes never borrow)
-    const uint32_t ibr = bytes4(ib);
-    const uint32_t yE = ((0x86848280u - ibr) >> (3 - SH)) & kStep;
-    const uint32_t yO = ((0x87858381u - ibr) >> (3 - SH)) & kStep;
+// ORed with its block's slot in the group << (SH + 4): `slot` for the piece's first block, +1
+// from each boundary on.  The boundaries (EP = elements per piece: none) are ib_in, a block
+// boundary inside the row before its end, and ib_end, the row's end; with a row's last block
+// at least EP long only one of them lies inside a piece (TRI false: one boundary, the smaller);
+// TRI: rows whose last block is shorter than a piece, where a piece can hold three blocks.
+// Nibble c of a row is the high nibble of its byte when c is even; W0 = bytes b .. b+3, W1 =
+// b+1 .. b+4 of the two loaded dwords.  ODD (odd n): the elements past the row's end sit one
+// nibble further on (the pad).
+template <int SH, bool ODD, bool TRI>
+__device__ __forceinline__ void piece_codes(uint32_t lo, uint32_t hi, int32_t b, int32_t c, uint32_t ib_in,
+                                            uint32_t ib_end, uint32_t slot, uint32_t& es, uint32_t& os) {
+    constexpr uint32_t kCode = 0x0F0F0F0Fu << SH, kStep = 0x01010101u << (SH + 4), kEP = 16u >> SH;
+    // bit SH + 4 of each byte of y(ib): the element lies at or past ib (0x80 + 2i - ib >= 0x80,
+    // bytes never borrow)
+    auto yE = [](uint32_t ib) { return ((0x86848280u - bytes4(ib)) >> (3 - SH)) & kStep; };
+    auto yO = [](uint32_t ib) { return ((0x87858381u - bytes4(ib)) >> (3 - SH)) & kStep; };
+    uint32_t sE, sO, eE, eO;  // slot increments; the bytes past the row's end
+    if constexpr (TRI) {
+        eE = yE(ib_end);
+        eO = yO(ib_end);
+        sE = eE + yE(ib_in);
+        sO = eO + yO(ib_in);
+    } else {
+        sE = yE(min(ib_in, ib_end));
+        sO = yO(min(ib_in, ib_end));
+        eE = ib_end < kEP ? sE : 0u;
+        eO = ib_end < kEP ? sO : 0u;
+    }
     const uint32_t sel = bytes4((uint32_t)b & 3u) + 0x03020100u;
     const uint32_t w0 = __builtin_amdgcn_perm(hi, lo, sel);
     const uint32_t w1 = __builtin_amdgcn_perm(hi, lo, sel + 0x01010101u);
@@ -1163,17 +1178,17 @@ __device__ __forceinline__ void piece_codes(uint32_t lo, uint32_t hi, int32_t b,
     if constexpr (ODD) {
         const uint32_t l1 = __builtin_amdgcn_alignbit(w1, w1, 32u - SH);
         const uint32_t E2 = O, O2 = odd ? l1 : h1;
-        const uint32_t kE = straddle ? yE - (yE >> 4) : 0u;  // the code bits of the bytes past the end
-        const uint32_t kO = straddle ? yO - (yO >> 4) : 0u;
+        const uint32_t kE = eE - (eE >> 4);  // the code bits of the bytes past the row's end
+        const uint32_t kO = eO - (eO >> 4);
         E = (E2 & kE) | (E & ~kE);
         O = (O2 & kO) | (O & ~kO);
     }
     const uint32_t rep = bytes4(slot << (SH + 4));
-    es = (E & kCode) | (rep + yE);
-    os = (O & kCode) | (rep + yO);
+    es = (E & kCode) | (rep + sE);
+    os = (O & kCode) | (rep + sO);
 }
 
-template <int DT, int MODE, bool ODD>
+template <int DT, int MODE, bool ODD, bool TRI>
 __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
     __shared__ __attribute__((aligned(256))) char ptbl[4 * kPieceTbl];
     const uint32_t lane = threadIdx.x & 63u;
@@ -1204,13 +1219,13 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
     for (int j = 0; j < 4; ++j) {
         // (c < 0: wave 0's first pieces, whose elements are block 0's or dropped)
         const uint32_t cu = (uint32_t)max(W.c[j], 0);
-        // the piece's first block (from g0) and the first element of the next block, if any
-        // (8: none): a boundary inside the row or the row's end, whichever comes first --
-        // the row end, when inside the piece, is the first (the last block holds >= 8)
+        // the piece's first block (from g0) and the elements where the next blocks start (8:
+        // none): a block boundary inside the row, the row's end (see piece_codes)
         const uint32_t tA = min(W.gr[j] + (cu >> 6), 59u);  // (59: lanes past the end)
-        const uint32_t ib = min(min(64u - (cu & 63u), A.n - cu), 8u);
+        const uint32_t to_blk = 64u - (cu & 63u), to_end = A.n - cu;
+        const uint32_t ib_in = to_blk < to_end ? min(to_blk, 8u) : 8u, ib_end = min(to_end, 8u);
         uint32_t es, os;
-        piece_codes<1, ODD>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib, A.n - cu < 8u, tA & 3u, es, os);
+        piece_codes<1, ODD, TRI>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib_in, ib_end, tA & 3u, es, os);
         const uint32_t base = region + ((tA >> 2) << 8);
         uint32_t p[4];
 #pragma unroll
@@ -1251,7 +1266,7 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
 // bits 2..5, slot x 64 in bits 6..7).
 constexpr uint32_t kPiece32Tbl = 12 * 256;  // a wave's tables: blocks 0 .. 23 (a wave touches <= 20)
 
-template <int MODE, bool ODD>
+template <int MODE, bool ODD, bool TRI>
 __global__ __launch_bounds__(kWg) void nf4_piece32_kernel(const PieceArgs A) {
     __shared__ __attribute__((aligned(256))) char ptbl[4 * kPiece32Tbl];
     const uint32_t lane = threadIdx.x & 63u;
@@ -1285,9 +1300,10 @@ __global__ __launch_bounds__(kWg) void nf4_piece32_kernel(const PieceArgs A) {
     for (int j = 0; j < 4; ++j) {
         const uint32_t cu = (uint32_t)max(W.c[j], 0);
         const uint32_t tA = min(W.gr[j] + (cu >> 6), 21u);  // (21: lanes past the end)
-        const uint32_t ib = min(min(64u - (cu & 63u), A.n - cu), 4u);
+        const uint32_t to_blk = 64u - (cu & 63u), to_end = A.n - cu;
+        const uint32_t ib_in = to_blk < to_end ? min(to_blk, 4u) : 4u, ib_end = min(to_end, 4u);
         uint32_t es, os;
-        piece_codes<2, ODD>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib, A.n - cu < 4u, tA & 1u, es, os);
+        piece_codes<2, ODD, TRI>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib_in, ib_end, tA & 1u, es, os);
         const uint32_t base = region + ((tA >> 1) << 8);
         uint32_t p[4];
 #pragma unroll
@@ -1554,24 +1570,33 @@ bool dense_eligible(const ChunkArgs& A, int32_t dtype) {
 
 // The piece kernels' shapes: tightly packed rows the dense form does not take (16-bit output:
 // n % 8 != 0, the output off 16-byte alignment or the packed weight off 4-byte alignment;
-// fp32: every such shape), rows of >= 512 elements whose last block holds >= 8 of them (a
-// piece then touches at most two blocks and a step at most one row end), and offsets below 2^31.
+// fp32: every such shape), rows of >= 512 elements (a step then crosses at most one row end),
+// and offsets below 2^31.
 bool piece_eligible(const ChunkArgs& A, int32_t dtype) {
     const uint64_t half = (A.n + 1u) / 2u;
     const uint64_t rows = A.out_elems / A.n;
     const uint64_t ob = dtype == NF4DQ_F32 ? 4u : 2u;
-    return A.stride == half && A.packed_len == rows * half && A.n >= 512u && (A.n % 64u == 0 || A.n % 64u >= 8u) &&
+    return A.stride == half && A.packed_len == rows * half && A.n >= 512u &&
            ob * (A.out_elems + 64u) < (uint64_t(1) << 31) && A.packed_len + 8u < (uint64_t(1) << 31);
+}
+
+template <int MODE, int DT, bool ODD, bool TRI>
+void launch_pieces_k(const PieceArgs& P, unsigned g, hipStream_t st) {
+    if constexpr (DT == NF4DQ_F32) hipLaunchKernelGGL((nf4_piece32_kernel<MODE, ODD, TRI>), dim3(g), dim3(kWg), 0, st, P);
+    else hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, ODD, TRI>), dim3(g), dim3(kWg), 0, st, P);
 }
 
 template <int MODE, int DT>
 void launch_pieces_dt(const PieceArgs& P, unsigned g, hipStream_t st) {
-    if constexpr (DT == NF4DQ_F32) {
-        if (P.n & 1u) hipLaunchKernelGGL((nf4_piece32_kernel<MODE, true>), dim3(g), dim3(kWg), 0, st, P);
-        else hipLaunchKernelGGL((nf4_piece32_kernel<MODE, false>), dim3(g), dim3(kWg), 0, st, P);
+    // TRI: the last block of a row is shorter than a piece (a piece can hold three blocks)
+    const uint32_t tail = P.n % 64u;
+    const bool tri = tail != 0u && tail < (DT == NF4DQ_F32 ? 4u : 8u);
+    if (P.n & 1u) {
+        if (tri) launch_pieces_k<MODE, DT, true, true>(P, g, st);
+        else launch_pieces_k<MODE, DT, true, false>(P, g, st);
     } else {
-        if (P.n & 1u) hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, true>), dim3(g), dim3(kWg), 0, st, P);
-        else hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, false>), dim3(g), dim3(kWg), 0, st, P);
+        if (tri) launch_pieces_k<MODE, DT, false, true>(P, g, st);
+        else launch_pieces_k<MODE, DT, false, false>(P, g, st);
     }
 }
 

@@ -4,9 +4,9 @@ n % 64 != 0, padded packed rows and unaligned pointers go through the kernels of
 csrc/nf4_dequant.hip.  Which instantiation a shape takes (launch_chunks):
 * nf4_chunk_dense_kernel -- 16-bit output, n % 8 == 0, packed rows of exactly 4 L bytes
   (L = chunks per row >= 64), 4-byte-aligned packed weight, 16-byte-aligned output;
-* nf4_piece_kernel -- 16-bit output of tight packed rows (exactly ceil(n / 2) bytes) that
-  the dense form does not take (n % 8 != 0, the output off 16-byte alignment or the
-  packed weight off 4-byte alignment), n >= 512, the last block of a row >= 8 elements:
+* nf4_piece_kernel / nf4_piece32_kernel -- tight packed rows (exactly ceil(n / 2) bytes)
+  of n >= 512 that the dense form does not take (16-bit: n % 8 != 0, the output off
+  16-byte alignment or the packed weight off 4-byte alignment; fp32: every such shape):
   aligned 16-byte output pieces in output order, each from the two packed dwords around
   its nibbles;
 * nf4_chunk_kernel<LW, SW> otherwise, with the load form LW = 4 (dword loads: packed
@@ -85,7 +85,7 @@ CASES = [
     (10, 1000, 2, 3, 3),      # the same, padded rows: LW 1, SW 4, L >= 64
     (3000, 2, 0, 0, 0),       # one chunk per row: 256 rows per wave (per-lane scale gathers)
     (300, 18, 5, 0, 1),
-    (129, 4100, 0, 0, 0),     # n % 64 == 4 (last block shorter than a piece): LW 4, SW 4, partial last wave
+    (129, 4100, 4, 0, 0),     # padded rows, n % 64 == 4: LW 4, SW 4, partial last wave
     # the piece kernel: even n (the stream runs across row ends), odd n (a pad nibble per
     # row), the shortest last block it takes (8: n % 64 == 8), n % 64 == 0 with the output
     # off alignment, output offsets up to 63 elements into the first line, one row
@@ -96,7 +96,12 @@ CASES = [
     (6, 4096, 0, 3, 5),
     (1, 600, 0, 0, 9),
     (70, 521, 0, 0, 0),       # rows of 521 (last block of 9): a step crosses a row end in most lanes
-    (9, 4096, 0, 1, 0),       # n % 64 == 0, aligned output, odd packed address (fp32: LW 1, SW 16)
+    (9, 4096, 0, 1, 0),       # n % 64 == 0, aligned output, odd packed address
+    # rows whose last block is shorter than a piece (three blocks in one piece)
+    (129, 4100, 0, 0, 0),
+    (9, 4097, 0, 1, 3),
+    (5, 577, 0, 2, 17),
+    (8, 515, 0, 3, 1),
 ]
 
 

@@ -14,6 +14,7 @@ launches behind a spin, as bench.py times its steps):
   pad_4096      4096x4096 with packed rows of 2052 bytes (the general form, dword loads)
   unal_4096     4096x4096 with the packed weight at an odd address (the piece kernel since round 6)
   oal_4096      4096x4096 with the output one element off 16-byte alignment
+  chunk_4100    4096x4100 (a row's last block holds 4 elements)
 --dtype f32 / f16: the output type (default bf16).
 --libs a,b: the same cases through other builds of the library (tools/_build/libnf4dq_<x>.so),
 interleaved, tagged "<x>:<case>".
@@ -39,7 +40,8 @@ from bench_configs import PEAK, alg_bytes, rotating_sets, rotation  # noqa: E402
 SHAPES = {"flat_4096": (4096, 4096, 0), "chunk_4096": (4096, 4096, _lib.CFG_CHUNKS),
           "chunk_4080": (4096, 4080, 0), "rows_4080": (4096, 4080, _lib.CFG_ROWS),
           "chunk_4095": (4096, 4095, 0), "chunk_4090": (4096, 4090, 0),
-          "pad_4096": (4096, 4096, 0), "unal_4096": (4096, 4096, 0), "oal_4096": (4096, 4096, 0)}
+          "pad_4096": (4096, 4096, 0), "unal_4096": (4096, 4096, 0), "oal_4096": (4096, 4096, 0),
+          "chunk_4100": (4096, 4100, 0)}
 # pad_4096: packed rows of 2052 bytes (n % 64 == 0 but not dense: the general form with
 # dword loads); unal_4096: the packed weight one byte into its allocation (alignbyte loads)
 PAD = {"pad_4096": 4}

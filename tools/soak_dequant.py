@@ -92,6 +92,9 @@ def main():
              Form("odd_f16", 777, 4095, O.F16, dev, orc, 16, ooff=3),          # the piece kernel
              Form("piece_even_bf16", 1024, 4090, O.BF16, dev, orc, 19, poff=2, ooff=45),
              Form("staged_f16", 777, 4095, O.F16, dev, orc, 20, pad=3, ooff=3),  # LDS-staged chunk form
+             Form("piece32_f32", 1000, 4090, O.F32, dev, orc, 21, poff=1, ooff=3),  # fp32 piece kernel
+             Form("tri_bf16", 1000, 4100, O.BF16, dev, orc, 22),                   # short last blocks
+             Form("padded_f32", 512, 4096, O.F32, dev, orc, 23, pad=4),
              Form("unaligned_bf16", 513, 1000, O.BF16, dev, orc, 17, poff=1, ooff=1),
              Form("single_bf16", 1000, 4080, O.BF16, dev, orc, 18, single=True)]
     # one Llama-3-8B layer through the batched entry (flat pieces in one launch)
