@@ -1047,7 +1047,8 @@ struct PieceArgs {
     uint32_t kb;            // the weight's first byte, from `packed` (0..3)
     uint32_t sa;            // the output's first element, from `line` (0..63)
     uint32_t elems;         // m * n
-    uint32_t n, half;       // columns; packed bytes per row = ceil(n / 2)
+    uint32_t n, half;       // columns; ceil(n / 2)
+    uint32_t stride;        // packed bytes per row (>= half; > half: padded rows)
     FastDiv nf, bpr;        // n; 64-column blocks per row
     uint32_t groups;        // ceil(bpr / 4)
     FastDiv nb, n2;         // ref: moduli of the absmax / nested-absmax indices
@@ -1066,33 +1067,37 @@ __device__ __forceinline__ uint32_t bytes4(uint32_t x) { return __builtin_amdgcn
 // all loads out first.  A step moves 64 EP <= 512 elements and rows are >= 512: at most one
 // row end per step, so every index advances by additions.  false: the wave lies wholly
 // past the end (it must return; no barrier follows in either kernel).
-template <uint32_t EP>
+// RE, how a piece's elements past its row's end are found: 0 = the next nibbles (tight rows,
+// even n: the stream runs on), 1 = one nibble further on (tight rows, odd n: the pad nibble),
+// 2 = the next row's first bytes, loaded separately (padded rows).
+template <uint32_t EP, int RE>
 struct PieceWave {
     int32_t fw;              // the wave's first element (< 0: wave 0)
     uint32_t c0, g0, gl;     // column of its first element in the matrix; its first / last block
     int32_t c[4], b[4];      // per step: column, byte of nibble c from `packed`
     uint32_t gr[4], lo[4], hi[4];  // per step: the row's first block from g0; the two dwords
+    uint32_t nb[4], lo2[4], hi2[4];  // RE 2, per step: the next row's first byte and its two dwords
 };
 
-template <uint32_t EP>
-__device__ __forceinline__ bool piece_wave(const PieceArgs& A, uint32_t kw, uint32_t lane, PieceWave<EP>& W) {
+template <uint32_t EP, int RE>
+__device__ __forceinline__ bool piece_wave(const PieceArgs& A, uint32_t kw, uint32_t lane, PieceWave<EP, RE>& W) {
     if (EP * kw >= A.sa + A.elems) return false;
     W.fw = (int32_t)(EP * kw) - (int32_t)A.sa;
     const uint32_t fwc = W.fw < 0 ? 0u : (uint32_t)W.fw;
     const uint32_t r0 = fdiv(fwc, A.nf);
     W.c0 = fwc - r0 * A.nf.d;
     const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)A.packed, 0, A.prange, kRsrcFlags);
-    uint32_t aj[4];
+    uint32_t aj[4], an[4];
     {
         int32_t c = (W.fw < 0 ? W.fw : (int32_t)W.c0) + (int32_t)(EP * lane);
-        uint32_t pb = A.kb + r0 * A.half;  // the row's first packed byte, from `packed`
-        uint32_t gb = 0u - (W.c0 >> 6);     // the row's first block, from g0
+        uint32_t pb = A.kb + r0 * A.stride;  // the row's first packed byte, from `packed`
+        uint32_t gb = 0u - (W.c0 >> 6);       // the row's first block, from g0
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (j) c += (int32_t)(64u * EP);
             const bool wrap = c >= (int32_t)A.n;  // (additions only: no multiply per step)
             c = wrap ? c - (int32_t)A.n : c;
-            pb = wrap ? pb + A.half : pb;
+            pb = wrap ? pb + A.stride : pb;
             gb = wrap ? gb + A.bpr.d : gb;
             W.c[j] = c;
             W.gr[j] = gb;
@@ -1100,6 +1105,15 @@ __device__ __forceinline__ bool piece_wave(const PieceArgs& A, uint32_t kw, uint
             // the range once unsigned -- the load returns 0)
             W.b[j] = (int32_t)pb + (c >> 1);
             aj[j] = (uint32_t)(W.b[j] & ~3);
+            if constexpr (RE == 2) {
+                // only a piece crossing its row's end loads the next row's first bytes
+                // (past the last row: beyond the range)
+                W.nb[j] = pb + A.stride;
+                an[j] = c > (int32_t)(A.n - EP) ? W.nb[j] & ~3u : kDrop;
+            } else {
+                W.nb[j] = W.lo2[j] = W.hi2[j] = 0u;  // (unused)
+                an[j] = 0u;
+            }
         }
     }
 #pragma unroll
@@ -1113,6 +1127,12 @@ __device__ __forceinline__ bool piece_wave(const PieceArgs& A, uint32_t kw, uint
         asm("" : "+v"(a4));
         W.lo[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, aj[j], 0, 0);
         W.hi[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, a4, 0, 0);
+        if constexpr (RE == 2) {
+            uint32_t n4 = an[j] + 4u;
+            asm("" : "+v"(n4));
+            W.lo2[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, an[j], 0, 0);
+            W.hi2[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, n4, 0, 0);
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
     W.g0 = r0 * A.bpr.d + (W.c0 >> 6);
@@ -1145,11 +1165,12 @@ __device__ __forceinline__ float piece_scale(const PieceArgs& A, uint32_t g0, ui
 // at least EP long only one of them lies inside a piece (TRI false: one boundary, the smaller);
 // TRI: rows whose last block is shorter than a piece, where a piece can hold three blocks.
 // Nibble c of a row is the high nibble of its byte when c is even; W0 = bytes b .. b+3, W1 =
-// b+1 .. b+4 of the two loaded dwords.  ODD (odd n): the elements past the row's end sit one
-// nibble further on (the pad).
-template <int SH, bool ODD, bool TRI>
+// b+1 .. b+4 of the two loaded dwords.  The elements from ib_end on come from the next row
+// as RE says (PieceWave); RE 2: its first bytes are the dword pair lo2 / hi2 around byte nb.
+template <int SH, int RE, bool TRI>
 __device__ __forceinline__ void piece_codes(uint32_t lo, uint32_t hi, int32_t b, int32_t c, uint32_t ib_in,
-                                            uint32_t ib_end, uint32_t slot, uint32_t& es, uint32_t& os) {
+                                            uint32_t ib_end, uint32_t slot, uint32_t lo2, uint32_t hi2,
+                                            uint32_t nb, uint32_t& es, uint32_t& os) {
     constexpr uint32_t kCode = 0x0F0F0F0Fu << SH, kStep = 0x01010101u << (SH + 4), kEP = 16u >> SH;
     // bit SH + 4 of each byte of y(ib): the element lies at or past ib (0x80 + 2i - ib >= 0x80,
     // bytes never borrow)
@@ -1175,9 +1196,20 @@ __device__ __forceinline__ void piece_codes(uint32_t lo, uint32_t hi, int32_t b,
     const uint32_t h1 = __builtin_amdgcn_alignbit(w1, w1, 4u - SH);
     const bool odd = (c & 1) != 0;
     uint32_t E = odd ? l0 : h0, O = odd ? h1 : l0;
-    if constexpr (ODD) {
-        const uint32_t l1 = __builtin_amdgcn_alignbit(w1, w1, 32u - SH);
-        const uint32_t E2 = O, O2 = odd ? l1 : h1;
+    if constexpr (RE != 0) {
+        uint32_t E2, O2;  // the codes the elements past the row's end take, in place
+        if constexpr (RE == 1) {  // one nibble further on
+            const uint32_t l1 = __builtin_amdgcn_alignbit(w1, w1, 32u - SH);
+            E2 = O;
+            O2 = odd ? l1 : h1;
+        } else {  // element i >= e = ib_end is column i - e of the next row (an even start)
+            const uint32_t wn = __builtin_amdgcn_perm(hi2, lo2, bytes4(nb & 3u) + 0x03020100u);
+            const uint32_t hn = __builtin_amdgcn_alignbit(wn, wn, 4u - SH);
+            const uint32_t ln = __builtin_amdgcn_alignbit(wn, wn, 32u - SH);
+            const uint32_t e = ib_end, eodd = e & 1u;
+            E2 = (eodd ? ln : hn) << ((8u * ((e + 1u) >> 1)) & 31u);  // (e = EP: masked out below)
+            O2 = (eodd ? hn : ln) << ((8u * (e >> 1)) & 31u);
+        }
         const uint32_t kE = eE - (eE >> 4);  // the code bits of the bytes past the row's end
         const uint32_t kO = eO - (eO >> 4);
         E = (E2 & kE) | (E & ~kE);
@@ -1188,13 +1220,13 @@ __device__ __forceinline__ void piece_codes(uint32_t lo, uint32_t hi, int32_t b,
     os = (O & kCode) | (rep + sO);
 }
 
-template <int DT, int MODE, bool ODD, bool TRI>
+template <int DT, int MODE, int RE, bool TRI>
 __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
     __shared__ __attribute__((aligned(256))) char ptbl[4 * kPieceTbl];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t kw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
-    PieceWave<8> W;
-    if (!piece_wave<8>(A, kw, lane, W)) return;  // (uniform)
+    PieceWave<8, RE> W;
+    if (!piece_wave<8, RE>(A, kw, lane, W)) return;  // (uniform)
     const float sb = piece_scale<MODE>(A, W.g0, W.gl, lane);
     const uint32_t region = (threadIdx.x >> 6) * kPieceTbl;
     {
@@ -1225,7 +1257,8 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
         const uint32_t to_blk = 64u - (cu & 63u), to_end = A.n - cu;
         const uint32_t ib_in = to_blk < to_end ? min(to_blk, 8u) : 8u, ib_end = min(to_end, 8u);
         uint32_t es, os;
-        piece_codes<1, ODD, TRI>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib_in, ib_end, tA & 3u, es, os);
+        piece_codes<1, RE, TRI>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib_in, ib_end, tA & 3u, W.lo2[j], W.hi2[j],
+                                W.nb[j], es, os);
         const uint32_t base = region + ((tA >> 2) << 8);
         uint32_t p[4];
 #pragma unroll
@@ -1266,13 +1299,13 @@ __global__ __launch_bounds__(kWg) void nf4_piece_kernel(const PieceArgs A) {
 // bits 2..5, slot x 64 in bits 6..7).
 constexpr uint32_t kPiece32Tbl = 12 * 256;  // a wave's tables: blocks 0 .. 23 (a wave touches <= 20)
 
-template <int MODE, bool ODD, bool TRI>
+template <int MODE, int RE, bool TRI>
 __global__ __launch_bounds__(kWg) void nf4_piece32_kernel(const PieceArgs A) {
     __shared__ __attribute__((aligned(256))) char ptbl[4 * kPiece32Tbl];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t kw = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u + (threadIdx.x >> 6)) * 256u);
-    PieceWave<4> W;
-    if (!piece_wave<4>(A, kw, lane, W)) return;  // (uniform)
+    PieceWave<4, RE> W;
+    if (!piece_wave<4, RE>(A, kw, lane, W)) return;  // (uniform)
     const float sb = piece_scale<MODE>(A, W.g0, W.gl, lane);
     const uint32_t region = (threadIdx.x >> 6) * kPiece32Tbl;
     if (lane < 24u) {
@@ -1303,7 +1336,8 @@ __global__ __launch_bounds__(kWg) void nf4_piece32_kernel(const PieceArgs A) {
         const uint32_t to_blk = 64u - (cu & 63u), to_end = A.n - cu;
         const uint32_t ib_in = to_blk < to_end ? min(to_blk, 4u) : 4u, ib_end = min(to_end, 4u);
         uint32_t es, os;
-        piece_codes<2, ODD, TRI>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib_in, ib_end, tA & 1u, es, os);
+        piece_codes<2, RE, TRI>(W.lo[j], W.hi[j], W.b[j], W.c[j], ib_in, ib_end, tA & 1u, W.lo2[j], W.hi2[j],
+                                W.nb[j], es, os);
         const uint32_t base = region + ((tA >> 1) << 8);
         uint32_t p[4];
 #pragma unroll
@@ -1568,36 +1602,40 @@ bool dense_eligible(const ChunkArgs& A, int32_t dtype) {
            aligned(A.out, 16) && A.chunks < (1u << 27);
 }
 
-// The piece kernels' shapes: tightly packed rows the dense form does not take (16-bit output:
-// n % 8 != 0, the output off 16-byte alignment or the packed weight off 4-byte alignment;
-// fp32: every such shape), rows of >= 512 elements (a step then crosses at most one row end),
-// and offsets below 2^31.
+// The piece kernels' shapes: rows of >= 512 elements (a step then crosses at most one row end)
+// the dense form does not take (16-bit output: n % 8 != 0, padded rows, the output off
+// 16-byte alignment or the packed weight off 4-byte alignment; fp32: every such shape), and
+// offsets below 2^31.
 bool piece_eligible(const ChunkArgs& A, int32_t dtype) {
     const uint64_t half = (A.n + 1u) / 2u;
     const uint64_t rows = A.out_elems / A.n;
     const uint64_t ob = dtype == NF4DQ_F32 ? 4u : 2u;
-    return A.stride == half && A.packed_len == rows * half && A.n >= 512u &&
+    // (padded 16-bit rows the chunk kernel stores whole, n % 8 == 0 and an aligned output,
+    // stay there: the same time, two loads fewer per piece; profiles/r06/chunk/s22)
+    if (A.stride != half && dtype != NF4DQ_F32 && A.n % 8u == 0 && aligned(A.out, 16)) return false;
+    return A.stride >= half && A.packed_len == rows * A.stride && A.n >= 512u &&
            ob * (A.out_elems + 64u) < (uint64_t(1) << 31) && A.packed_len + 8u < (uint64_t(1) << 31);
 }
 
-template <int MODE, int DT, bool ODD, bool TRI>
+template <int MODE, int DT, int RE, bool TRI>
 void launch_pieces_k(const PieceArgs& P, unsigned g, hipStream_t st) {
-    if constexpr (DT == NF4DQ_F32) hipLaunchKernelGGL((nf4_piece32_kernel<MODE, ODD, TRI>), dim3(g), dim3(kWg), 0, st, P);
-    else hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, ODD, TRI>), dim3(g), dim3(kWg), 0, st, P);
+    if constexpr (DT == NF4DQ_F32) hipLaunchKernelGGL((nf4_piece32_kernel<MODE, RE, TRI>), dim3(g), dim3(kWg), 0, st, P);
+    else hipLaunchKernelGGL((nf4_piece_kernel<DT, MODE, RE, TRI>), dim3(g), dim3(kWg), 0, st, P);
+}
+
+template <int MODE, int DT, int RE>
+void launch_pieces_re(const PieceArgs& P, unsigned g, hipStream_t st) {
+    // TRI: the last block of a row is shorter than a piece (a piece can hold three blocks)
+    const uint32_t tail = P.n % 64u;
+    if (tail != 0u && tail < (DT == NF4DQ_F32 ? 4u : 8u)) launch_pieces_k<MODE, DT, RE, true>(P, g, st);
+    else launch_pieces_k<MODE, DT, RE, false>(P, g, st);
 }
 
 template <int MODE, int DT>
 void launch_pieces_dt(const PieceArgs& P, unsigned g, hipStream_t st) {
-    // TRI: the last block of a row is shorter than a piece (a piece can hold three blocks)
-    const uint32_t tail = P.n % 64u;
-    const bool tri = tail != 0u && tail < (DT == NF4DQ_F32 ? 4u : 8u);
-    if (P.n & 1u) {
-        if (tri) launch_pieces_k<MODE, DT, true, true>(P, g, st);
-        else launch_pieces_k<MODE, DT, true, false>(P, g, st);
-    } else {
-        if (tri) launch_pieces_k<MODE, DT, false, true>(P, g, st);
-        else launch_pieces_k<MODE, DT, false, false>(P, g, st);
-    }
+    if (P.stride != P.half) launch_pieces_re<MODE, DT, 2>(P, g, st);  // padded rows
+    else if (P.n & 1u) launch_pieces_re<MODE, DT, 1>(P, g, st);
+    else launch_pieces_re<MODE, DT, 0>(P, g, st);
 }
 
 template <int MODE>
@@ -1616,6 +1654,7 @@ int launch_pieces(const ChunkArgs& A, int32_t dtype, hipStream_t st) {
     P.elems = (uint32_t)A.out_elems;
     P.n = A.n;
     P.half = (A.n + 1u) / 2u;
+    P.stride = A.stride;
     P.nf = make_fastdiv(A.n);
     P.bpr = A.bpr;
     P.groups = A.groups;

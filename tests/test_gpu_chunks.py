@@ -4,13 +4,14 @@ n % 64 != 0, padded packed rows and unaligned pointers go through the kernels of
 csrc/nf4_dequant.hip.  Which instantiation a shape takes (launch_chunks):
 * nf4_chunk_dense_kernel -- 16-bit output, n % 8 == 0, packed rows of exactly 4 L bytes
   (L = chunks per row >= 64), 4-byte-aligned packed weight, 16-byte-aligned output;
-* nf4_piece_kernel / nf4_piece32_kernel -- tight packed rows (exactly ceil(n / 2) bytes)
-  of n >= 512 that the dense form does not take (16-bit: n % 8 != 0, the output off
-  16-byte alignment or the packed weight off 4-byte alignment; fp32: every such shape):
-  aligned 16-byte output pieces in output order, each from the two packed dwords around
-  its nibbles;
-* nf4_chunk_kernel<LW, SW> otherwise, with the load form LW = 4 (dword loads: packed
-  weight and row stride 4-byte aligned) or 1 (two aligned dwords per chunk joined with
+* nf4_piece_kernel / nf4_piece32_kernel -- rows of n >= 512 that the dense form does not
+  take (16-bit: n % 8 != 0, the output off 16-byte alignment or the packed weight off
+  4-byte alignment, with tight or padded rows; fp32: every such shape): aligned 16-byte
+  output pieces in output order, each from the two packed dwords around its nibbles
+  (padded rows: a piece crossing its row's end loads the next row's first bytes apart);
+* nf4_chunk_kernel<LW, SW> otherwise (rows < 512; 16-bit padded rows stored whole), with
+  the load form LW = 4 (dword loads: packed weight and row stride 4-byte aligned) or 1
+  (two aligned dwords per chunk joined with
   v_alignbyte: any alignment), and the store form SW = 16 (one 16-byte store per chunk,
   or two for fp32: n % 8 == 0 (fp32: n % 4 == 0) and a 16-byte-aligned output) or 4
   (16-bit outputs staged through LDS and written as aligned 16-byte pieces, the span's
@@ -67,11 +68,16 @@ def _ref_call(dev, p, a1, a2, m, n, dt, p_off=0, o_elem_off=0, flags=None):
 CASES = [
     (37, 1000, 0, 0, 0),      # n % 8 == 0, rows of exactly 4 L bytes, L >= 64: the dense form
     (5, 4080, 0, 0, 0),       # (the dense form)
-    (33, 1000, 4, 0, 0),      # padded rows: LW 4 (dword loads), SW 16 (16-byte chunk stores)
+    (33, 1000, 4, 0, 0),      # padded rows, n % 8 == 0: LW 4, SW 16 (fp32: the piece kernel)
+    (33, 1002, 3, 0, 0),      # padded rows, n % 8 != 0: the piece kernel, next row's bytes loaded apart
+    (33, 504, 4, 0, 0),       # padded rows < 512: LW 4 (dword loads), SW 16 (16-byte chunk stores), L < 64
+    (33, 508, 4, 0, 0),       # LW 4, L >= 64: 16-bit SW 4 (staged), fp32 SW 16
     (9, 4080, 0, 0, 1),       # output off 16-byte alignment, tight rows: the piece kernel (fp32: LW 4, SW 4)
-    (9, 4080, 4, 0, 1),       # the same with padded rows: LW 4, SW 4 (staged)
+    (9, 4080, 4, 0, 1),       # the same with padded rows (piece kernel)
+    (9, 510, 4, 0, 1),        # rows < 512, L >= 64, output off alignment: LW 4, SW 4 (staged)
     (9, 1002, 0, 0, 0),       # n % 8 == 2, stride 501: the piece kernel (fp32: LW 1, SW 4)
-    (9, 1002, 1, 0, 0),       # n % 8 == 2, padded to stride 502: LW 1, SW 4 (staged)
+    (9, 1002, 1, 0, 0),       # n % 8 == 2, padded to stride 502 (piece kernel)
+    (9, 506, 1, 0, 0),        # stride 254, L >= 64: LW 1, SW 4 (staged)
     (3, 6, 0, 0, 0),          # L = 1: LW 1, SW 4, per-step row division
     (7, 77, 0, 0, 0),         # odd n (stride 39): LW 1, SW 4
     (1, 1, 0, 0, 0),
@@ -82,10 +88,12 @@ CASES = [
     (6, 256, 0, 1, 0),        # odd packed pointer: LW 1
     (6, 256, 0, 2, 1),        # output one element off 16-byte alignment: SW 4
     (10, 1000, 0, 3, 3),      # piece kernel: odd packed address, output 3 elements off
-    (10, 1000, 2, 3, 3),      # the same, padded rows: LW 1, SW 4, L >= 64
+    (10, 1000, 2, 3, 3),      # the same, padded rows (piece kernel)
+    (10, 510, 2, 3, 3),       # rows < 512: LW 1, SW 4, L >= 64
     (3000, 2, 0, 0, 0),       # one chunk per row: 256 rows per wave (per-lane scale gathers)
     (300, 18, 5, 0, 1),
-    (129, 4100, 4, 0, 0),     # padded rows, n % 64 == 4: LW 4, SW 4, partial last wave
+    (129, 4100, 4, 0, 0),     # padded rows, n % 64 == 4 (piece kernel, three blocks)
+    (129, 509, 1, 0, 0),      # rows < 512, stride 256: LW 4, SW 4, partial last wave
     # the piece kernel: even n (the stream runs across row ends), odd n (a pad nibble per
     # row), the shortest last block it takes (8: n % 64 == 8), n % 64 == 0 with the output
     # off alignment, output offsets up to 63 elements into the first line, one row

@@ -5,11 +5,11 @@ chunk kernel, a wave of the last workgroup lying wholly past the end of the matr
 its row index from its unclamped first chunk, gathered single-quant scales past the
 absmax rows and wrote its (empty) staged span past the output.  This module sweeps that
 class of shape on purpose, for every load / store form of the chunk kernels
-(csrc/nf4_dequant.hip: the dense form; the general form with dword loads or alignbyte
-dword pairs, whole-chunk 16-byte stores or LDS staging, rows of >= 64 chunks or fewer)
-and of the piece kernel (16-bit outputs of tight rows in output order: even and odd n,
-odd packed and output offsets, rows whose last block is shorter than a piece; its fp32
-form), in both scale modes:
+(csrc/nf4_dequant.hip: the dense form; the general form -- rows < 512 -- with dword
+loads or alignbyte dword pairs, whole-chunk 16-byte stores or LDS staging, rows of >= 64
+chunks or fewer) and of the piece kernel (outputs in 16-byte pieces in output order: even
+and odd n, padded rows, odd packed and output offsets, rows whose last block is shorter
+than a piece; its fp32 form), in both scale modes:
 
 * m is chosen so that the last workgroup (4 waves x 256 four-byte chunks, or 256 16-byte
   output pieces) holds 1, 2 and 3 waves wholly past the end, and 0 as the control;
@@ -37,11 +37,11 @@ pytestmark = pytest.mark.gpu
 # name: (n, extra packed bytes per row, packed byte offset, output element offset, dtypes, kernel)
 FORMS = {
     "dense": (1000, 0, 0, 0, ("bf16", "f16"), "chunk"),              # n % 8 == 0, rows of exactly 4 L bytes
-    "dword_whole": (1000, 4, 0, 0, ("bf16", "f32"), "chunk"),        # padded rows: dword loads, 16-byte stores
-    "alignbyte_whole": (1000, 4, 1, 0, ("f16", "f32"), "chunk"),     # odd packed address, padded rows: dword pairs + v_alignbyte
-    "dword_staged": (1007, 4, 0, 0, ("bf16", "f16", "f32"), "chunk"),  # padded odd-n rows (stride 508): LDS-staged
-    "alignbyte_staged": (1029, 2, 0, 0, ("bf16", "f32"), "chunk"),   # padded rows, stride 517: both
-    "unaligned_out": (1000, 4, 0, 1, ("bf16",), "chunk"),            # padded rows, output one element off: staged
+    "dword_whole": (504, 4, 0, 0, ("bf16", "f32"), "chunk"),         # padded rows: dword loads, 16-byte stores
+    "alignbyte_whole": (504, 4, 1, 0, ("f16", "f32"), "chunk"),      # odd packed address, padded rows: dword pairs + v_alignbyte
+    "dword_staged": (509, 1, 0, 0, ("bf16", "f16", "f32"), "chunk"),  # odd n, stride 256, L = 64: LDS-staged
+    "alignbyte_staged": (510, 2, 0, 0, ("bf16", "f32"), "chunk"),    # stride 257, L = 64: both
+    "unaligned_out": (504, 4, 0, 1, ("bf16",), "chunk"),             # padded rows, output one element off: staged
     "short_rows": (200, 0, 0, 0, ("bf16", "f32"), "chunk"),          # L = 25 < 64 chunks: per-step row division
     "short_odd": (77, 0, 0, 0, ("f16",), "chunk"),                   # L = 10, odd n: staged, dword pairs
     # the piece kernel (16-bit output, tight rows the dense form does not take):
@@ -52,11 +52,14 @@ FORMS = {
     "piece_min_block": (520, 0, 3, 5, ("bf16",), "piece"),           # last block of 8 elements, rows of 520
     "piece_unal_packed": (1000, 0, 1, 0, ("f16",), "piece"),         # n % 8 == 0, aligned output, odd packed address
     "piece_tri": (1029, 0, 0, 0, ("bf16", "f16"), "piece"),          # last block of 5: three blocks in a piece
+    "piece_padded": (1002, 4, 0, 0, ("bf16",), "piece"),             # padded rows: the next row's bytes apart
+    "piece_padded_odd": (1007, 3, 1, 5, ("f16",), "piece"),
     # its fp32 form (4-element pieces; every tight fp32 shape the flat kernel does not take)
     "piece32_odd": (1007, 0, 1, 5, ("f32",), "piece32"),
     "piece32_even": (1002, 0, 0, 0, ("f32",), "piece32"),
     "piece32_aligned_n": (1000, 0, 0, 0, ("f32",), "piece32"),       # n % 8 == 0, everything aligned
     "piece32_tri": (1027, 0, 1, 3, ("f32",), "piece32"),             # last block of 3: three blocks in a piece
+    "piece32_padded": (1002, 2, 0, 3, ("f32",), "piece32"),
 }
 
 

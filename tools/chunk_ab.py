@@ -15,6 +15,7 @@ launches behind a spin, as bench.py times its steps):
   unal_4096     4096x4096 with the packed weight at an odd address (the piece kernel since round 6)
   oal_4096      4096x4096 with the output one element off 16-byte alignment
   chunk_4100    4096x4100 (a row's last block holds 4 elements)
+  padodd_4090   4096x4090 with packed rows of 2048 bytes (padded, n % 8 != 0)
 --dtype f32 / f16: the output type (default bf16).
 --libs a,b: the same cases through other builds of the library (tools/_build/libnf4dq_<x>.so),
 interleaved, tagged "<x>:<case>".
@@ -41,10 +42,10 @@ SHAPES = {"flat_4096": (4096, 4096, 0), "chunk_4096": (4096, 4096, _lib.CFG_CHUN
           "chunk_4080": (4096, 4080, 0), "rows_4080": (4096, 4080, _lib.CFG_ROWS),
           "chunk_4095": (4096, 4095, 0), "chunk_4090": (4096, 4090, 0),
           "pad_4096": (4096, 4096, 0), "unal_4096": (4096, 4096, 0), "oal_4096": (4096, 4096, 0),
-          "chunk_4100": (4096, 4100, 0)}
+          "chunk_4100": (4096, 4100, 0), "padodd_4090": (4096, 4090, 0)}
 # pad_4096: packed rows of 2052 bytes (n % 64 == 0 but not dense: the general form with
 # dword loads); unal_4096: the packed weight one byte into its allocation (alignbyte loads)
-PAD = {"pad_4096": 4}
+PAD = {"pad_4096": 4, "padodd_4090": 3}
 UNAL = {"unal_4096": 1}
 OOFF = {"oal_4096": 1}  # output element offset
 

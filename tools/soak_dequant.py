@@ -91,7 +91,8 @@ def main():
              Form("padded_bf16", 1024, 4096, O.BF16, dev, orc, 15, pad=4),
              Form("odd_f16", 777, 4095, O.F16, dev, orc, 16, ooff=3),          # the piece kernel
              Form("piece_even_bf16", 1024, 4090, O.BF16, dev, orc, 19, poff=2, ooff=45),
-             Form("staged_f16", 777, 4095, O.F16, dev, orc, 20, pad=3, ooff=3),  # LDS-staged chunk form
+             Form("padded_odd_f16", 777, 4095, O.F16, dev, orc, 20, pad=3, ooff=3),  # piece kernel, padded rows
+             Form("staged_bf16", 3000, 510, O.BF16, dev, orc, 24, ooff=1),         # LDS-staged chunk form
              Form("piece32_f32", 1000, 4090, O.F32, dev, orc, 21, poff=1, ooff=3),  # fp32 piece kernel
              Form("tri_bf16", 1000, 4100, O.BF16, dev, orc, 22),                   # short last blocks
              Form("padded_f32", 512, 4096, O.F32, dev, orc, 23, pad=4),
