@@ -50,8 +50,9 @@
 #if defined(ABL_NOX)
 #define NF4_ABL_X_ON 0
 #endif
-#if defined(ABL_NOXR)  // the persistent / streaming body's x fragments from registers (no LDS read; wrong results)
-#define NF4_ABL_XFRAG(smem_, off_) (u32x4{(off_), (off_) ^ 0x3F803F80u, (off_) + 0x3C003C00u, 0x3F803F80u})
+#if defined(ABL_NOXR)  // the persistent / streaming body's x fragments from registers: one constant
+// fragment, materialised once outside the loops (no LDS read, no VALU per step; wrong results)
+#define NF4_ABL_XFRAG(smem_, off_) (u32x4{0x3F803F80u, 0x3E803F00u, 0x3F803E80u, 0x3F003F80u})
 #endif
 #if defined(ABL_NOMMA)
 #define NF4_ABL_MMA_ON 0
