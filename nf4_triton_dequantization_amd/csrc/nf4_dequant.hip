@@ -32,10 +32,14 @@
 //    walk several tiles in the software-pipelined loop.
 //  * batched: up to NF4DQ_BATCH_MAX matrices per launch in the kernel
 //    arguments; a wave finds its matrix by scanning scalar tile offsets.
-//  * "chunk" kernels: any other shape (partial blocks, padded rows, odd n,
+//  * "chunk" kernels (round 5): any other shape (partial blocks, padded rows, odd n,
 //    unaligned pointers) -- the flat tile with rows cut out of the stream and
 //    one LDS table per scale block of the wave; the one-thread-per-byte "rows"
 //    kernel only past their 32-bit index limits.
+//  * "piece" kernels (round 6): of those, every row of >= 512 elements the chunk
+//    kernel could not store whole (n % 8 != 0, a misaligned output or packed
+//    weight, fp32 output), in OUTPUT order: 16-byte output pieces stored straight
+//    from registers, the irregularity moved to the packed loads.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
