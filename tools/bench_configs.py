@@ -17,6 +17,8 @@ big  128256x8192 NF4->bf16 (Llama-3-70B lm_head size: 525 MB packed, past one bu
      descriptor -- two row pieces in one launch).
 odd  4096x4080 NF4->bf16: n % 64 != 0 (every row ends in a partial 64-block), so the
      matrix takes the chunk kernel (its dense form), not the flat kernel; same method as c4.
+piece 4096x4090 NF4->bf16 and ->fp32, 4096x4100 NF4->bf16 (n % 8 != 0; a 4-element last
+     block): the piece kernels (round 6), same method as c4, every output verified.
 bnb  4096x4096 NF4->bf16 with bitsandbytes semantics (nf4_dequant_bnb: code2[A1] * A2
      + offset, flat blocks), same method as c4; its algorithmic bytes
      add the 1 KiB nested code book.
@@ -265,7 +267,7 @@ def run_bnb(name, m, n, reps, dev, steps=64):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c3,c3b,c4,c5,big,odd,bnb")
+    ap.add_argument("--configs", default="c3,c3b,c4,c5,big,odd,piece,bnb")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--layers", type=int, default=32)
     args = ap.parse_args()
@@ -295,6 +297,12 @@ def main():
     if "odd" in todo:
         print(json.dumps(run_single("odd 4096x4080 (n % 64 != 0: the chunk kernel)", 4096, 4080, torch.bfloat16,
                                     _lib.BF16, args.reps, dev)), flush=True)
+        torch.cuda.empty_cache()
+    if "piece" in todo:
+        for n, dt, code in ((4090, torch.bfloat16, _lib.BF16), (4090, torch.float32, _lib.F32),
+                            (4100, torch.bfloat16, _lib.BF16)):
+            print(json.dumps(run_single(f"piece 4096x{n} (n % 8 != 0: the piece kernel)", 4096, n, dt, code,
+                                        args.reps, dev)), flush=True)
         torch.cuda.empty_cache()
     if "bnb" in todo:
         print(json.dumps(run_bnb("bnb-semantics 4096x4096 NF4->bf16", 4096, 4096, args.reps, dev)), flush=True)
