@@ -167,14 +167,17 @@ def test_rows_kernel_still_matches(coracle, gpu, dt):
         _check(buf, start, m, n, dt, want, f"rows {m}x{n} {dt}")
 
 
-def test_drop_in_takes_the_chunk_kernel_for_odd_widths(coracle, gpu):
-    """The drop-in API on a BASELINE-sized matrix with n % 64 != 0."""
+@pytest.mark.parametrize("n,dt", [(4080, "bf16"), (4090, "bf16"), (4095, "f16"), (4100, "bf16"), (4090, "f32")])
+def test_drop_in_takes_the_chunk_and_piece_kernels_for_odd_widths(coracle, gpu, n, dt):
+    """The drop-in API on BASELINE-sized matrices with n % 64 != 0: 4080 the chunk kernel's
+    dense form, the others the piece kernels (odd n: a pad nibble per row; 4100: a 4-element
+    last block), bit for bit against the C oracle at full size."""
     import nf4_triton_dequantization as N
     from _helpers import make_module
 
-    m, n = 4096, 4080
-    p, a1, a2, _ = O.golden_case_inputs(m, n, 4080, {"stride": n // 2})
-    want = coracle.dequant_ref(p, a1, a2, m, n, O.BF16)
-    out = N.triton_dequantize_nf4(make_module(p, a1, a2, m, n, "bf16", gpu))
+    m = 4096
+    p, a1, a2, _ = O.golden_case_inputs(m, n, n, {"stride": (n + 1) // 2})
+    want = coracle.dequant_ref(p, a1, a2, m, n, DT_CODE[dt])
+    out = N.triton_dequantize_nf4(make_module(p, a1, a2, m, n, dt, gpu))
     assert out.shape == (m, n) and out.is_contiguous()
-    assert_bits_equal(out_bits(out), want, "bf16", "drop-in 4096x4080")
+    assert_bits_equal(out_bits(out), want, dt, f"drop-in {m}x{n} {dt}")
