@@ -130,11 +130,12 @@ int nf4_dequant_bnb_single(const uint8_t* packed, const float* absmax, int64_t n
  * policies measured slower and were removed, profiles/r01/tune_sweep.log,
  * profiles/r02/x4_direct/).  blocks_per_cu: grid cap per CU (0 = one wave per
  * tile, no cap; capped grids walk tiles persistently).  flags: 0, or one of
- * NF4DQ_CFG_CHUNKS (the matrix goes through the chunk kernel -- the kernel of
- * every shape the flat kernel does not take: n % 64 != 0, padded rows, unaligned
- * pointers -- even when it is flat-eligible) or NF4DQ_CFG_ROWS (through the
- * one-thread-per-byte general kernel, which otherwise runs only past the chunk
- * kernel's 32-bit index limits); for tests and tuning.  Other bits: NF4DQ_ERR_ARG.
+ * NF4DQ_CFG_CHUNKS (the matrix goes through the path of every shape the flat
+ * kernel does not take -- n % 64 != 0, padded rows, unaligned pointers: the chunk
+ * kernels and, since round 6, the piece kernels -- even when it is flat-eligible) or
+ * NF4DQ_CFG_ROWS (through the one-thread-per-byte general kernel, which otherwise
+ * runs only past the chunk kernel's 32-bit index limits); for tests and tuning.
+ * Other bits: NF4DQ_ERR_ARG.
  * (Absmax-line and page-translation prefetches were tried as flags and measured
  * no better than 1 %, profiles/r03/c5/; removed.) */
 #define NF4DQ_CFG_ROWS 1

@@ -64,7 +64,7 @@ class LaunchCfg(ctypes.Structure):
 
 
 CFG_ROWS = 1    # NF4DQ_CFG_ROWS: the one-thread-per-byte general kernel
-CFG_CHUNKS = 2  # NF4DQ_CFG_CHUNKS: the chunk kernel, even for a flat-eligible matrix
+CFG_CHUNKS = 2  # NF4DQ_CFG_CHUNKS: the chunk / piece kernels' path, even for a flat-eligible matrix
 
 
 GEMM_K128 = 1
