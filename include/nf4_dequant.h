@@ -204,6 +204,12 @@ int nf4_gemm_ref(const void* x, int64_t M, const uint8_t* packed, int64_t packed
  * never the library's choice (slower than the persistent kernel at every measured
  * shape) and no longer ships; a cfg naming it is rejected with NF4DQ_ERR_ARG. */
 #define NF4DQ_GEMM_SK 6
+/* NF4DQ_GEMM_GEMV: the decode GEMV (M == 1, K % 2048 == 0, K <= 16384, absmax not
+ * wrapping inside a row): no MFMA; a lane dots 32 consecutive exact weights of a row
+ * with x on the VALU.  waves 8/16 per workgroup, depth = rows per row group 1/2/4,
+ * ksplit 1, strips = workgroups per CU 0/1/2 (0 = 1).  The library's choice at M = 1
+ * for launches of up to 4096 columns. */
+#define NF4DQ_GEMM_GEMV 7
 typedef struct nf4_gemm_cfg {
     int32_t kernel;
     int32_t waves;

@@ -73,6 +73,7 @@ GEMM_PERSIST = 3
 GEMM_XS = 4
 GEMM_XR = 5
 GEMM_SK = 6  # retired in round 6: rejected with ERR_ARG
+GEMM_GEMV = 7  # the decode GEMV (M = 1, K % 2048 == 0)
 
 
 GEMM_GROUP_MAX = 8

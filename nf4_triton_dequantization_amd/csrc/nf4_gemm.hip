@@ -109,6 +109,18 @@ nf4_gemm_cfg default_gemm_cfg(int64_t M, int64_t N, int64_t K) {
     return nonpersist_cfg(M, N, K);
 }
 
+// M = 1: the decode GEMV (nf4_gemm_launch_gemv.hip) where it beats the persistent kernel:
+// up to 4096 columns (profiles/r06/gemm/s29_gemv_ab.jsonl, s30_gemv_ab.jsonl, one box each:
+// 4096^2 5.77-5.99 vs 6.33 us, 4096 x 14336 10.25-10.61 vs 11.16-11.62); wider launches
+// stay persistent (14336 x 4096: 11.6 vs 10.5; grouped q/k/v 7.6 vs 7.3).  N = all columns
+// of the launch.  The caller falls back to default_gemm_cfg when it cannot run (absmax
+// wrapping inside a row).
+static bool gemv_choice(int64_t M, int64_t N, int64_t K, nf4_gemm_cfg* c) {
+    if (M != 1 || K % 2048 || K > 16384 || N > 4096) return false;
+    *c = nf4_gemm_cfg{NF4DQ_GEMM_GEMV, 16, 1, 1, 0};
+    return true;
+}
+
 // Dynamic LDS of the persistent kernel: x slice, zero block, two partial-sum
 // sets, the held outputs (16-bit finished values; fp32 partials when K is split).
 bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
@@ -151,6 +163,12 @@ bool valid_gemm_cfg(const nf4_gemm_cfg& c, int64_t M, int64_t N, int64_t K) {
     // choice -- 13.1-15.1 vs 10.6 us on 14336x4096 at M = 1,
     // profiles/r04/gemm/sk_depth_vs_persist.jsonl -- and was removed in round 6: its
     // number is rejected like any unknown kernel (git history holds the source)
+    if (c.kernel == NF4DQ_GEMM_GEMV) {
+        if (M != 1 || K % 2048 || K > 16384 || c.ksplit != 1) return false;
+        if (c.waves != 8 && c.waves != 16) return false;
+        if (c.depth != 1 && c.depth != 2 && c.depth != 4) return false;
+        return c.strips >= 0 && c.strips <= 2 && N % c.depth == 0;
+    }
     if (c.kernel == NF4DQ_GEMM_XS) {
         if (c.waves != 4 && c.waves != 8) return false;
         if (c.depth != 2 && c.depth != 4 && c.depth != 8) return false;
@@ -180,6 +198,12 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
     if (M > NF4DQ_GEMM_MAX_M || N % 64 || K % kChunkK || packed_len != N * (K / 2)) return NF4DQ_ERR_SHAPE;
     if ((size_t)(N / 16) * 4 > kCounterBytes) return NF4DQ_ERR_TOO_LARGE;
     if (packed_len >= (int64_t(1) << 31) || M * K * 2 >= (int64_t(1) << 31)) return NF4DQ_ERR_TOO_LARGE;
+    nf4_gemm_cfg gv{};
+    if (!cfgp && gemv_choice(M, N, K, &gv)) {
+        const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
+        const int rc = launch_gemv(&h, 1, x, M, K, dtype, gv, st);
+        if (rc != NF4DQ_ERR_ARG) return rc;  // else absmax wraps inside a row: the next choice
+    }
     nf4_gemm_cfg cfg = cfgp ? *cfgp : default_gemm_cfg(M, N, K);
     if (cfg.kernel == 0) {
         const nf4_gemm_cfg d = default_gemm_cfg(M, N, K);
@@ -209,6 +233,7 @@ static int gemm_impl(const void* x, int64_t M, const uint8_t* packed, int64_t pa
         return launch_stream(&h, 1, x, M, K, dtype, cfg, workspace, st);
     }
     const HostMat h{packed, packed_len, absmax_q, nb, absmax2, n2, y, N};
+    if (cfg.kernel == NF4DQ_GEMM_GEMV) return launch_gemv(&h, 1, x, M, K, dtype, cfg, st);
     if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(&h, 1, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_XR) return launch_xr(&h, 1, x, M, K, dtype, cfg, workspace, st);
     return launch_k128(&h, 1, x, M, K, dtype, cfg, workspace, st);
@@ -256,7 +281,17 @@ static int gemm_grouped_impl(const void* x, int64_t M, int64_t K, const nf4_gemm
     for (int i = 0; i < count; ++i)
         h[i] = HostMat{mats[i].packed, mats[i].packed_len, mats[i].absmax_q, mats[i].nb, mats[i].absmax2,
                        mats[i].n2, mats[i].y, mats[i].N};
+    nf4_gemm_cfg gv{};
+    if (!cfgp && gemv_choice(M, ntot, K, &gv)) {
+        bool empty = false;
+        for (int i = 0; i < count; ++i) empty = empty || mats[i].N == 0;
+        if (!empty) {
+            const int rc = launch_gemv(h, count, x, M, K, dtype, gv, st);
+            if (rc != NF4DQ_ERR_ARG) return rc;  // else absmax wraps inside a row: the next choice
+        }
+    }
     if (cfg.kernel == NF4DQ_GEMM_K128) return launch_k128(h, count, x, M, K, dtype, cfg, workspace, st);
+    if (cfg.kernel == NF4DQ_GEMM_GEMV) return launch_gemv(h, count, x, M, K, dtype, cfg, st);
     if (cfg.kernel == NF4DQ_GEMM_XS) return launch_xs(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_XR) return launch_xr(h, count, x, M, K, dtype, cfg, workspace, st);
     if (cfg.kernel == NF4DQ_GEMM_PERSIST) {

@@ -31,6 +31,8 @@ int launch_xr(const HostMat* mats, int count, const void* x, int64_t M, int64_t 
               const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st);
 int launch_k128(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
                 const nf4_gemm_cfg& cfg, void* workspace, hipStream_t st);
+int launch_gemv(const HostMat* mats, int count, const void* x, int64_t M, int64_t K, int32_t dtype,
+                const nf4_gemm_cfg& cfg, hipStream_t st);
 
 }  // namespace nf4gemm
 

@@ -94,11 +94,12 @@ def test_wrapping_absmax_and_leading_dims(coracle, gpu):
     _check(y.reshape(6, N), xb, W, "bf16")
 
 
-@pytest.mark.parametrize("M", [4, 12, 16])
+@pytest.mark.parametrize("M", [1, 4, 12, 16])
 def test_library_choice_falls_back_when_absmax_wraps_in_a_row(coracle, gpu, M):
-    """At these M the library picks the persistent kernel (K-sliced above 8 rows), which
-    needs absmax without wrap inside a row; with a wrapping absmax (nb = 7, n2 = 3) it must
-    fall back to the next choice -- single weight and grouped -- not fail."""
+    """At these M the library picks the decode GEMV (M = 1) or the persistent kernel
+    (K-sliced above 8 rows), which need absmax without wrap inside a row; with a wrapping
+    absmax (nb = 7, n2 = 3) it must fall back to the next choice -- single weight and
+    grouped -- not fail."""
     from nf4_triton_dequantization_amd import nf4_linear, nf4_linear_grouped
 
     K = 4096
@@ -304,6 +305,35 @@ def test_xr_multi_strip_workgroups(coracle, gpu, dt, M, K, kpw, spw):
     _check(y, xb, W, dt)
 
 
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (448, 14336), (64, 2048), (192, 16384), (14336, 4096)])
+def test_gemv_every_decomposition(coracle, gpu, dt, N, K):
+    """The decode GEMV (NF4DQ_GEMM_GEMV, M = 1): every waves / rows-per-group / grid form
+    against the float64 oracle, outputs pre-filled with NaN (every row written)."""
+    from nf4_triton_dequantization_amd import _lib
+
+    L = _lib.lib()
+    packed, a1, a2 = O.make_inputs(N, K, seed=N * 5 + K, a2_kind="normal")
+    W = coracle.dequant_ref(packed, a1, a2, N, K, O.BF16 if dt == "bf16" else O.F16)
+    t = (torch.from_numpy(packed).to(gpu), torch.from_numpy(a1).to(gpu), torch.from_numpy(a2).to(gpu))
+    xt, xb = _x_bits(1, K, dt, seed=K + 3)
+    x = xt.to(gpu)
+    code = _lib.BF16 if dt == "bf16" else _lib.F16
+    xf, wf = _bits_to_f64(xb, dt), _bits_to_f64(W, dt)
+    ref = torch.from_numpy(xf @ wf.T).to(gpu)
+    tol = torch.from_numpy(_tol(xf @ wf.T, np.abs(xf) @ np.abs(wf).T, dt)).to(gpu)
+    y = torch.empty((1, N), dtype=x.dtype, device=gpu)
+    for waves in (8, 16):
+        for rows in (1, 2, 4):
+            for wgs in (0, 1, 2):  # workgroups per CU
+                cfg = _lib.GemmCfg(_lib.GEMM_GEMV, waves, rows, 1, wgs)
+                y.fill_(float("nan"))
+                rc = _gemm_cfg_call(L, _lib, x, t, y, code, N, K, cfg)
+                assert rc == 0, (waves, rows, wgs, rc)
+                bad = ((y.double() - ref).abs() > tol) | torch.isnan(y)
+                assert not bool(bad.any()), (waves, rows, wgs, int(bad.sum()))
+
+
 def test_invalid_decompositions_rejected(gpu):
     from nf4_triton_dequantization_amd import _lib
 
@@ -313,7 +343,9 @@ def test_invalid_decompositions_rejected(gpu):
     F = 0x1000
     for cfg in [(_lib.GEMM_STREAM, 6, 4, 1, 1), (_lib.GEMM_STREAM, 8, 3, 1, 1), (_lib.GEMM_STREAM, 8, 4, 1, 3),
                 (_lib.GEMM_STREAM, 4, 4, 1, 8), (_lib.GEMM_STREAM, 8, 4, 0, 1), (_lib.GEMM_STREAM, 8, 4, 99, 1),
-                (_lib.GEMM_K128, 16, 2, 1, 1), (_lib.GEMM_K128, 8, 2, 1, 3), (7, 8, 4, 1, 1)]:
+                (_lib.GEMM_K128, 16, 2, 1, 1), (_lib.GEMM_K128, 8, 2, 1, 3), (9, 8, 4, 1, 1),
+                (_lib.GEMM_GEMV, 8, 3, 1, 1), (_lib.GEMM_GEMV, 4, 1, 1, 1), (_lib.GEMM_GEMV, 16, 1, 2, 1),
+                (_lib.GEMM_GEMV, 16, 1, 1, 3)]:
         c = _lib.GemmCfg(*cfg)
         assert L.nf4_gemm_ref_cfg(F, 1, F, 64 * 2048, F, 64 * 64, F, 16, F, _lib.BF16, 64, 4096, F, 1 << 30,
                                   ctypes.byref(c), None) == _lib.ERR_ARG, cfg
