@@ -46,8 +46,10 @@ def tol(ref, mag, dt):
 
 
 def random_cfg(rng, M, N, K):
-    """A drawn configuration of one of the five kernels (may be invalid: skipped)."""
-    k = int(rng.integers(1, 6))  # (6, the balanced kernel, was retired in round 6)
+    """A drawn configuration of one of the six kernels (may be invalid: skipped)."""
+    k = int(rng.choice([1, 2, 3, 4, 5, 7]))  # (6, the balanced kernel, was retired in round 6)
+    if k == _lib.GEMM_GEMV:  # the decode GEMV: M = 1, K % 2048 == 0 (else rejected)
+        return _lib.GemmCfg(k, int(rng.choice([8, 16])), int(rng.choice([1, 2, 4])), 1, int(rng.choice([0, 1, 2])))
     waves = int(rng.choice([4, 8, 16]))
     depth = int(rng.choice([1, 2, 4, 8]))
     strips = int(rng.choice([1, 2, 4]))
@@ -68,6 +70,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--seconds", type=float, default=500.0)
     ap.add_argument("--cfg-rate", type=float, default=0.25, help="share of cases that also run a drawn configuration")
+    ap.add_argument("--gemv-rate", type=float, default=0.0,
+                    help="share of cases at M = 1 with K % 2048 == 0 and N <= 4096 (the decode GEMV's domain)")
     ap.add_argument("--boundary-rate", type=float, default=0.1,
                     help="share of cases drawn from the default-rule boundary shapes (large N, K = 14336)")
     args = ap.parse_args()
@@ -90,6 +94,8 @@ def main():
             M = int(rng.choice([1, 8, 9, 16, 17, 24, 25, 32]))
             N, K = [(1024, 4096), (4096, 4096), (8192, 4096), (14336, 4096), (24576, 4096), (28672, 4096),
                     (4096, 14336), (1024, 14336)][int(rng.integers(0, 8))]
+        if rng.random() < args.gemv_rate:
+            M, N, K = 1, 64 * int(rng.integers(1, 65)), 2048 * int(rng.integers(1, 9))
         dt = "bf16" if rng.random() < 0.6 else "f16"
         nb_full = N * K // 64
         ov = {"a2_kind": "normal" if rng.random() < 0.5 else "uniform"}
