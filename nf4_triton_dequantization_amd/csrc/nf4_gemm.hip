@@ -13,6 +13,7 @@ using namespace nf4gemm;
 // profiles/r04/gemm/sweep_gemm_m1_12.jsonl, sweep_gemm_m16_32.jsonl: the default is
 // the fastest or within 2 % of it except where noted below).  N = all columns of the
 // launch (a grouped launch passes the sum).
+//  * M = 1, N <= 4096, K % 2048 == 0: the decode GEMV (round 6, gemv_choice below).
 //  * M <= 8: the persistent kernel whenever x[M][K] fits its LDS (the streaming
 //    kernel if absmax wraps inside a row), strips by width.
 //  * 8 < M <= 16: the persistent kernel with K slices; the register-resident

@@ -27,6 +27,8 @@
 //    a register ring of weight chunks, pair-table dequant (see its comments).
 //  * nf4_gemm_persist_kernel -- the streaming body with one workgroup per CU
 //    walking strip groups (M <= 16), the ring running on across groups.
+// (The seventh, the decode GEMV for M = 1 -- no MFMA, the exact weights dotted with x on
+// the VALU -- lives with its launcher in nf4_gemm_launch_gemv.hip.)
 // All use the same k permutation on A and B fragments (a lane's packed dword
 // is exactly its MFMA B fragment of one step), so no shuffle is needed.  K
 // slices over workgroups (ksplit > 1) write fp32 partials to a workspace slab;
